@@ -1,0 +1,240 @@
+"""Benchmark: preconditioned-GMRES iterations/s (+ CSR SpMV achieved HBM GB/s) on the C3
+20M-row synthetic Vlasov operator (BASELINE.json configs[3], the north_star's target), one
+rank per MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step = one full solve: x0 = 0 -> ||b - A x|| <= 1e-8 ||b|| with GMRES(20) + block-Jacobi(8)
+(SURVEY.md §8d).  value = inner (Arnoldi) iterations of the K timed solves / the max-over-ranks
+wall time of those solves.  The problem is fixed as N grows (strong scaling; rows sharded in
+contiguous x-slabs, RCCL halo exchange + all-reduce).  Operator, RHS and BJ inverses are built
+on the device before the timed region; b and x live in HBM (torch tensors passed through the
+C-ABI as device pointers).
+
+Printed: ONE JSON line on rank 0 (the driver's contract), with `roofline` (the dominant
+kernel, timed live with HIP events on the context's stream) and `cpu_baseline` (SciPy, the
+north_star's reference scipy.sparse path, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vt-precondition_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+CONFIGS = {  # name -> (dim, shape, fp32)   SURVEY.md Appendix A
+    "C1": (2, (1250, 800), False),
+    "C2": (2, (6250, 800), False),
+    "C3": (2, (25_000, 800), False),
+    "C4": (4, (200, 125, 50, 40), True),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def spmv_bytes(nnz, n, fp32):
+    # B_spmv = 12 nnz + 4 (n+1) + 8 n (x once) + 8 n (y)   (fp32 values: 8 nnz)   SURVEY §8d
+    return (8 if fp32 else 12) * nnz + 4 * (n + 1) + 16 * n
+
+
+def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit):
+    """SciPy 1.15.3 (the reference scipy.sparse path) on the host cores, bounded sample."""
+    import numpy as np
+    import scipy.sparse as sp
+
+    from oracle import twin
+    try:
+        from threadpoolctl import threadpool_info
+        blas_threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    except Exception:
+        blas_threads = 1
+    ip, ix, d = A_host
+    n = ip.shape[0] - 1
+    A = sp.csr_matrix((d, ix, ip), shape=(n, n))
+    x = twin.rhs(n, seed=0xC0FFEE)
+    A @ x
+    t = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        A @ x
+    t_spmv = (time.perf_counter() - t) / reps
+    Binv = twin.bj_inverse_numpy(ip, ix, d, n, bs)
+    s = twin.scipy_gmres(A, b, Binv, rtol=rtol, inner_limit=inner_limit)
+    return {
+        "value": s.inner_iters / s.seconds,
+        "unit": "iters/s",
+        "cores": int(blas_threads),
+        "kind": "reference",
+        "sample": (f"scipy.sparse.linalg.gmres(restart=20, M=BJ({bs}) LinearOperator) on the same "
+                   f"{cfg_name} operator/RHS, first {s.inner_iters} inner iterations (one restart "
+                   f"cycle, legacy maxiter bound) in {s.seconds:.1f} s; csr_matvec is single-threaded, "
+                   f"np.dot uses {blas_threads} BLAS threads; host cpus in affinity: "
+                   f"{len(os.sched_getaffinity(0))}"),
+        "spmv_gbs": spmv_bytes(ip[-1], n, d.dtype == np.float32) / t_spmv / 1e9,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--bs", type=int, default=8)
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--restart", type=int, default=20)
+    ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-inner", type=int, default=20)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+
+    import vtkrylov as vk
+    ctx = vk.Context(local)
+    if world > 1:
+        uid = vk.Context.unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        ctx.comm_init(rank, world, bytes(t.tolist()))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    dim, shape, fp32 = CONFIGS[args.config]
+    params = vk.vlasov_params(dim, shape, fp32=fp32)
+    n_glob = int(np.prod(shape))
+    align = shape[-1] if dim == 2 else shape[-1] * shape[-2] * shape[-3]   # x-slab boundaries
+    offsets = vk.partition_rows(n_glob, world, align) if world > 1 else None
+    t0 = time.time()
+    A = vk.vlasov_operator(params, ctx=ctx, offsets=offsets)
+    M = vk.block_jacobi(A, args.bs)
+    b_host = vk.rhs_splitmix(n_glob, r0=A.row_begin, r1=A.row_end)
+    b = torch.from_numpy(b_host).to(dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.time() - t0:.1f}s: n_local={A.n_local} nnz_local={A.nnz} halo={A.n_halo}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def solve():
+        x, info = vk.gmres(A, b, rtol=args.rtol, restart=args.restart, M=M)
+        return x, info, vk.last_stats()
+
+    for _ in range(args.warmup):
+        _, info, st = solve()
+    barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    iters = 0
+    infos = []
+    for _ in range(args.steps):
+        x, info, st = solve()
+        iters += st.inner_iters
+        infos.append(info)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # true residual of the last solve, on the device (vtk_spmv), reduced over ranks
+    r = b - A @ x
+    rn2 = torch.tensor([float(torch.dot(r, r).item()), float(torch.dot(b, b).item())], dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(rn2)
+    rel_res = float((rn2[0] / rn2[1]).sqrt())
+
+    # ---- SpMV kernel, live HIP-event timing on the context's stream ----------------------
+    import ctypes as C
+    lib = vk._abi.lib()
+    xs = torch.from_numpy(vk.rhs_splitmix(n_glob, seed=0xC0FFEE, r0=A.row_begin, r1=A.row_end)).to(dev)
+    ys = torch.empty_like(xs)
+    torch.cuda.synchronize()
+    stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        vk._abi.check(lib.vtk_spmv(A.handle, C.c_void_p(xs.data_ptr()), C.c_void_p(ys.data_ptr()), 1))
+    ctx.synchronize()
+    ev0.record(stream)
+    for _ in range(args.spmv_reps):
+        vk._abi.check(lib.vtk_spmv(A.handle, C.c_void_p(xs.data_ptr()), C.c_void_p(ys.data_ptr()), 1))
+    ev1.record(stream)
+    ev1.synchronize()
+    t_spmv = ev0.elapsed_time(ev1) / 1e3 / args.spmv_reps
+    B = spmv_bytes(A.nnz, A.n_local, fp32)
+    spmv_gbs = B / t_spmv / 1e9
+
+    ms = elapsed / args.steps * 1e3
+    out = {
+        "metric": "precond-GMRES iters/sec + CSR SpMV achieved-HBM-GB/s, 1/2/4/8 MI355X",
+        "value": iters / elapsed,
+        "unit": "iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if not fp32 else "f32-values/f64",
+        "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
+        "config": {"workload": f"{args.config}: GMRES({args.restart})+BJ({args.bs}) to rtol={args.rtol}, "
+                               f"n={n_glob}, row-sharded over {world} GPU(s)",
+                   "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
+                   "bs": args.bs, "rtol": args.rtol, "parallelism": f"row-slab x{world}"},
+        "inner_iters_per_solve": iters / args.steps,
+        "info": infos,
+        "true_rel_residual": rel_res,
+        "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6,
+                 "bytes": B},
+        "roofline": {"kernel": "k_spmv (CSR-stream, plain)", "bound": "hbm", "achieved": spmv_gbs,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": spmv_gbs / HBM_PEAK_GBS,
+                     "traffic": None},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            A_host = A.download()
+            out["cpu_baseline"] = cpu_baseline(args.config, A_host, b_host, args.bs, args.rtol,
+                                               args.cpu_inner)
+        except Exception as e:  # reported, never silently replaced
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def params_nnz(dim, shape):
+    import numpy as np
+    n = int(np.prod(shape))
+    if dim == 2:
+        return 5 * n - 2 * shape[0]
+    return 9 * n - 2 * (n // shape[2]) - 2 * (n // shape[3])
+
+
+if __name__ == "__main__":
+    main()

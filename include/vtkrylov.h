@@ -1,0 +1,158 @@
+/* vtkrylov.h — C-ABI of libvtkrylov.so, the MI355X-native preconditioned-Krylov path.
+ *
+ * Boundary.  jwang1x/VT-precondition has no solver, no FFI and no plugin
+ * interface (the reference is Python provisioning scripts only).  The
+ * entry points below replace the calls the north_star's "reference scipy.sparse path"
+ * makes — the reference-side binding a maintainer adds is the ctypes stub in
+ * INTEGRATION.md (vtkrylov/_abi.py in this repo) — and each declaration names the SciPy
+ * interface it stands in for:
+ *   vtk_csr_create      <- scipy.sparse.csr_matrix((data, indices, indptr), shape)
+ *                          (scipy/sparse/_compressed.py _cs_matrix.__init__)
+ *   vtk_spmv            <- csr_matrix @ x -> _matmul_vector (scipy/sparse/_compressed.py:518-530)
+ *   vtk_bjacobi_create  <- numpy.linalg.inv on the bs x bs diagonal blocks
+ *   vtk_bjacobi_apply   <- LinearOperator(matvec=einsum('bij,bj->bi'))
+ *   vtk_gmres           <- scipy.sparse.linalg.gmres(A, b, x0, rtol=, atol=, restart=,
+ *                          maxiter=, M=) (scipy/sparse/linalg/_isolve/iterative.py:582-841)
+ * The config/entry layer the reference does have (XML node lookups, ini_info.py:72-118;
+ * step objects with main(), hypervisor.py:589-594) is mirrored in Python by
+ * vt-precondition_amd/vtconfig + vtsetup, which call this ABI through ctypes.
+ *
+ * Conventions: every int-returning function returns VTK_OK (0) or a negative vtk_status;
+ * nothing throws or aborts across the boundary; vtk_last_error() explains the last failure
+ * of a context (vtk_last_error(NULL, ...) the last failure of a context-free call).
+ * Handles are opaque, owned by the caller, freed by the matching *_destroy.  Host arrays
+ * passed in stay owned by the caller (they are copied).  A handle is not thread-safe:
+ * one context per thread and device, one rank per process.
+ */
+#ifndef VTKRYLOV_H
+#define VTKRYLOV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VTK_ABI_VERSION 1
+
+typedef struct vtk_ctx vtk_ctx;
+typedef struct vtk_csr vtk_csr;
+typedef struct vtk_prec vtk_prec;
+
+typedef enum {
+    VTK_OK = 0,
+    VTK_ERR_ARG = -1,       /* bad argument / shape / index                        */
+    VTK_ERR_HIP = -2,       /* HIP runtime error                                   */
+    VTK_ERR_RCCL = -3,      /* RCCL error                                          */
+    VTK_ERR_SINGULAR = -4,  /* singular diagonal block (numpy.linalg.LinAlgError)  */
+    VTK_ERR_NOMEM = -5,     /* host or device allocation failed                    */
+    VTK_ERR_STATE = -6,     /* call not valid in this state (e.g. comm not set)    */
+    VTK_ERR_NODEVICE = -7   /* no HIP device: the product has no CPU fallback      */
+} vtk_status;
+
+typedef enum { VTK_PTR_HOST = 0, VTK_PTR_DEVICE = 1 } vtk_ptr_kind;
+
+typedef enum {
+    VTK_ORTH_MGS = 0,   /* modified Gram-Schmidt, SciPy's order (iterative.py:755-759)       */
+    VTK_ORTH_CGS2 = 1   /* classical GS + one re-orthogonalisation: 2 reductions per step   */
+} vtk_orth;
+
+/* Synthetic Vlasov operator parameters. */
+typedef struct {
+    int dim;            /* 1, 2 or 4                                   */
+    int fp32;           /* 1: values stored as float32 (C4)            */
+    int64_t shape[4];   /* (n) | (Nx, Nv) | (Nx, Ny, Nvx, Nvy)          */
+    double vmax, E0, nu, alpha, cfl;
+} vtk_vlasov_params;
+
+typedef struct {
+    int64_t inner_iters;   /* Arnoldi steps over all restart cycles (SciPy's inner_iter)  */
+    int64_t restarts;      /* restart cycles run                                          */
+    double presid;         /* last preconditioned residual estimate                       */
+    double rnorm;          /* last true residual ||b - A x||                              */
+    double bnorm;          /* ||b||                                                       */
+    double atol_eff;       /* max(atol, rtol*||b||)  (_get_atol_rtol, iterative.py:19)    */
+    double t_solve;        /* seconds, device work of the solve (host wall, synced)       */
+    double bytes_moved;    /* algorithmic HBM bytes of the solve           */
+    int breakdown;         /* 1 if the last cycle hit h1 <= eps*h0                        */
+    int orth;              /* vtk_orth used                                               */
+} vtk_stats;
+
+/* ---- library ------------------------------------------------------------------------ */
+int vtk_abi_version(void);
+const char *vtk_status_string(int status);
+/* last error message of ctx (or of the last context-free call when ctx == NULL) */
+int vtk_last_error(vtk_ctx *ctx, char *buf, size_t len);
+
+/* ---- host-only helpers (no GPU required) -------------------------------------------- */
+/* operator assembly (Appendix A) */
+int vtk_vlasov_size(const vtk_vlasov_params *p, int64_t *n, int64_t *nnz);
+/* rows [r0, r1): indptr has r1-r0+1 entries starting at 0; indices are global columns;
+ * data is double[] or float[] per p->fp32; buffers sized for the row block's nnz */
+int vtk_vlasov_generate(const vtk_vlasov_params *p, int64_t r0, int64_t r1, int32_t *indptr,
+                        int32_t *indices, void *data);
+/* b[i - r0] = 2 * ((splitmix64(seed + i) >> 11) * 2^-53) - 1   */
+int vtk_rhs_splitmix(uint64_t seed, int64_t r0, int64_t r1, double *b);
+/* contiguous row partition: offsets[world+1], boundaries multiples of align, balanced by
+ * nnz when indptr (global, n+1 entries) is given, else by rows */
+int vtk_partition_rows(int64_t n, const int32_t *indptr, int world, int align, int64_t *offsets);
+/* Halo plan of one rank's row block.  In: local CSR with GLOBAL column
+ * indices, the partition offsets.  Out: local_indices (nnz entries; owned column c ->
+ * c - row_begin, halo column -> n_local + position in halo_cols), halo_cols (global ids,
+ * sorted ascending, so grouped by owner rank) and halo_count_per_rank[world].  Pass
+ * halo_cols == NULL to query *n_halo first. */
+int vtk_halo_plan(int64_t n_global, const int64_t *offsets, int world, int rank,
+                  int64_t nnz, const int32_t *indices, int32_t *local_indices,
+                  int64_t *n_halo, int64_t *halo_cols, int64_t *halo_count_per_rank);
+
+/* ---- device context / communicator ---------------------------------------------------- */
+int vtk_device_count(int *count);
+int vtk_ctx_create(int hip_device, vtk_ctx **out);      /* owns one hipStream_t */
+void vtk_ctx_destroy(vtk_ctx *ctx);
+int vtk_ctx_stream(vtk_ctx *ctx, void **hip_stream);    /* the stream all work runs on */
+int vtk_ctx_synchronize(vtk_ctx *ctx);
+/* rank 0 creates the 128-byte RCCL unique id; the caller broadcasts it (any transport) */
+int vtk_comm_unique_id(void *out128);
+int vtk_comm_init(vtk_ctx *ctx, int rank, int world, const void *rccl_unique_id);
+int vtk_comm_info(vtk_ctx *ctx, int *rank, int *world);
+
+/* ---- operator ------------------------------------------------------------------------ */
+/* Row block [offsets[rank], offsets[rank+1]) of an n_global x n_global CSR matrix with
+ * GLOBAL column indices.  offsets has world+1 entries (NULL when world == 1).  Arrays are
+ * host or device memory per ptr_kind and are copied. */
+int vtk_csr_create(vtk_ctx *ctx, int64_t n_global, const int64_t *offsets, int64_t nnz_local,
+                   const int32_t *indptr, const int32_t *indices, const void *data,
+                   int data_is_fp32, int ptr_kind, vtk_csr **out);
+/* generate this rank's rows of the Vlasov operator directly into device memory */
+int vtk_csr_create_vlasov(vtk_ctx *ctx, const vtk_vlasov_params *p, const int64_t *offsets,
+                          vtk_csr **out);
+int vtk_csr_info(vtk_csr *A, int64_t *n_global, int64_t *row_begin, int64_t *row_end,
+                 int64_t *nnz_local, int64_t *n_halo);
+/* copy this rank's CSR back (indices GLOBAL), host memory */
+int vtk_csr_download(vtk_csr *A, int32_t *indptr, int32_t *indices, void *data);
+void vtk_csr_destroy(vtk_csr *A);
+
+/* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged
+ * internally over RCCL when world > 1).  Bit-identical to csr_matvec (serial row sums). */
+int vtk_spmv(vtk_csr *A, const double *x, double *y, int ptr_kind);
+
+/* ---- block-Jacobi preconditioner ------------------------------------------------------- */
+int vtk_bjacobi_create(vtk_csr *A, int block_size, vtk_prec **out);
+/* export the block inverses: (n_local + bs - 1) / bs blocks of bs*bs doubles, row-major */
+int vtk_bjacobi_inverse(vtk_prec *M, double *inv, int ptr_kind);
+int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int ptr_kind);
+void vtk_prec_destroy(vtk_prec *M);
+
+/* ---- solver --------------------------------------------------------------------------- */
+/* scipy.sparse.linalg.gmres semantics (iterative.py:582-841, callback=None): restarted,
+ * left-preconditioned GMRES(restart); maxiter counts restart cycles (<= 0: 10 n); x holds
+ * x0 on entry and the solution on exit; info = 0 on convergence else maxiter. */
+int vtk_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, double atol,
+              int restart, int64_t maxiter, int ptr_kind, int *info, vtk_stats *stats);
+int vtk_gmres_set_orth(vtk_ctx *ctx, int orth);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VTKRYLOV_H */

@@ -1,0 +1,169 @@
+"""Generate the committed golden fixtures from SciPy 1.15.3 / NumPy 2.2.6 (the north_star's
+"reference scipy.sparse path"; /root/reference itself has no numerical code).
+
+    python tests/golden/make_golden.py            # small fixtures + C1/C2/C3 summaries
+    python tests/golden/make_golden.py --c4       # also hash the 445.5M-nnz C4 operator
+
+Outputs (all data, no code):
+  golden_small.npz  — vectors for C0, S2, S4, S4F, a ragged random CSR, GMRES edge cases
+  golden_large.json — SHA-256 of the C1..C4 CSR byte streams, ||A·1||, SciPy GMRES summary
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.abspath(os.path.join(HERE, "..", "..")))
+
+from oracle import twin  # noqa: E402
+
+X_SEED = 0xC0FFEE
+
+
+def ragged_csr(seed=1234, n=3000):
+    """Random CSR with empty rows, one very long row and one dense-ish band; canonical."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 12, size=n)
+    lens[rng.choice(n, 50, replace=False)] = 0          # empty rows
+    lens[7] = 2500                                       # one wave-per-row candidate
+    lens[1500] = 700
+    rows = np.repeat(np.arange(n), lens)
+    cols = np.concatenate([rng.choice(n, size=l, replace=False) for l in lens])
+    vals = rng.standard_normal(rows.shape[0])
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    A.sum_duplicates()
+    A.sort_indices()
+    # make it comfortably non-singular (diagonal dominance) for BJ/GMRES on it
+    A = A + sp.diags(np.abs(A).sum(axis=1).A1 + 1.0)
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    return A
+
+
+def small(out):
+    import scipy.sparse as sp  # noqa: F401
+    g = {}
+    for name in ["C0", "S2", "S4", "S4F"]:
+        p = twin.CONFIGS[name]
+        ip, ix, d = twin.generate(p)
+        A = twin.scipy_csr(ip, ix, d, p.n)
+        x = twin.rhs(p.n, seed=X_SEED)
+        b = twin.rhs(p.n)
+        g[f"{name}/spmv_y"] = A @ x
+        g[f"{name}/ones_y"] = A @ np.ones(p.n)
+        inv = twin.bj_inverse_numpy(ip, ix, d, p.n, 8)
+        g[f"{name}/bj8_z"] = twin.bj_apply_numpy(inv, b, p.n)
+        if name != "C0":
+            g[f"{name}/bj8_inv"] = inv
+        s = twin.scipy_gmres(A, b, inv, rtol=1e-8)
+        g[f"{name}/gmres_x"] = s.x
+        g[f"{name}/gmres_meta"] = np.array([s.info, s.inner_iters, s.true_resid, s.b_norm])
+        print(name, "info", s.info, "inner", s.inner_iters, "res", s.true_resid / s.b_norm)
+    # GMRES edge cases on S2 / C0
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = twin.generate(p)
+    A = twin.scipy_csr(ip, ix, d, p.n)
+    b = twin.rhs(p.n)
+    inv = twin.bj_inverse_numpy(ip, ix, d, p.n, 8)
+    from scipy.sparse.linalg import gmres
+
+    def case(key, **kw):
+        M = kw.pop("M", None)
+        bb = kw.pop("b", b)
+        AA = kw.pop("A", A)
+        count = [0]
+        x, info = gmres(AA, bb, M=M, callback=lambda _: count.__setitem__(0, count[0] + 1),
+                        callback_type="pr_norm", **kw)
+        g[f"edge/{key}/x"] = x
+        g[f"edge/{key}/meta"] = np.array([info, count[0], np.linalg.norm(bb - AA @ x),
+                                          np.linalg.norm(bb)])
+        print("edge", key, info, count[0])
+
+    Mbj = twin.bj_operator(inv, p.n)
+    case("noprec", rtol=1e-8)
+    x0 = 0.1 * twin.rhs(p.n, seed=7)
+    g["edge/x0/x0"] = x0
+    case("x0", M=Mbj, x0=x0, rtol=1e-10)
+    case("restart5_maxiter3", M=Mbj, rtol=1e-12, restart=5, maxiter=3)
+    case("bzero", M=Mbj, b=np.zeros(p.n), rtol=1e-8)
+    case("atol", M=Mbj, rtol=0.0, atol=1e-3)
+    case("restart40", M=Mbj, rtol=1e-9, restart=40)
+    # ragged random CSR: SpMV and BJ(4) only (general-CSR path: empty rows, long rows)
+    R = ragged_csr()
+    g["ragged/indptr"] = R.indptr.astype(np.int32)
+    g["ragged/indices"] = R.indices.astype(np.int32)
+    g["ragged/data"] = R.data
+    xr = twin.rhs(R.shape[0], seed=X_SEED)
+    g["ragged/spmv_y"] = R @ xr
+    invr = twin.bj_inverse_numpy(R.indptr, R.indices, R.data, R.shape[0], 4)
+    g["ragged/bj4_z"] = twin.bj_apply_numpy(invr, twin.rhs(R.shape[0]), R.shape[0])
+    # partial last block: n not divisible by bs (n = 3000, bs = 7)
+    invr7 = twin.bj_inverse_numpy(R.indptr, R.indices, R.data, R.shape[0], 7)
+    g["ragged/bj7_z"] = twin.bj_apply_numpy(invr7, twin.rhs(R.shape[0]), R.shape[0])
+    Mr = twin.bj_operator(invr, R.shape[0])
+    case_b = twin.rhs(R.shape[0])
+    count = [0]
+    xr_s, info = gmres(R, case_b, M=Mr, rtol=1e-10, callback=lambda _: count.__setitem__(0, count[0] + 1),
+                       callback_type="pr_norm")
+    g["ragged/gmres_x"] = xr_s
+    g["ragged/gmres_meta"] = np.array([info, count[0], np.linalg.norm(case_b - R @ xr_s),
+                                       np.linalg.norm(case_b)])
+    np.savez_compressed(out, **g)
+    print("wrote", out, os.path.getsize(out), "bytes")
+
+
+def large(out, with_c4):
+    res = {}
+    if os.path.exists(out):
+        with open(out) as f:
+            res = json.load(f)
+    res["_provenance"] = ("SciPy 1.15.3 / NumPy 2.2.6 in the build container; operator = "
+                          "oracle/twin.py (SURVEY.md Appendix A); script tests/golden/make_golden.py")
+    names = ["C1", "C2", "C3"] + (["C4"] if with_c4 else [])
+    for name in names:
+        p = twin.CONFIGS[name]
+        t = time.time()
+        h = twin.csr_sha256(p)
+        h["n"] = p.n
+        assert h["nnz"] == p.nnz
+        print(name, "hash", time.time() - t, "s")
+        res.setdefault(name, {}).update({"sha256": h})
+    # C1: ||A 1||, SpMV of the x-seed vector (norm + checksum), SciPy GMRES+BJ(8) summary
+    p = twin.CONFIGS["C1"]
+    ip, ix, d = twin.generate(p)
+    A = twin.scipy_csr(ip, ix, d, p.n)
+    b = twin.rhs(p.n)
+    x = twin.rhs(p.n, seed=X_SEED)
+    y = A @ x
+    inv = twin.bj_inverse_numpy(ip, ix, d, p.n, 8)
+    t = time.time()
+    s = twin.scipy_gmres(A, b, inv, rtol=1e-8)
+    print("C1 gmres", time.time() - t, s.info, s.inner_iters)
+    res["C1"].update({
+        "A_ones_norm2": float(np.linalg.norm(A @ np.ones(p.n))),
+        "spmv_y_norm2": float(np.linalg.norm(y)),
+        "spmv_y_sha256": __import__("hashlib").sha256(y.tobytes()).hexdigest(),
+        "gmres_bj8": {"rtol": 1e-8, "restart": 20, "info": s.info, "inner_iters": s.inner_iters,
+                      "x_norm2": float(np.linalg.norm(s.x)), "true_resid": s.true_resid,
+                      "b_norm2": s.b_norm, "x_first8": s.x[:8].tolist()},
+    })
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print("wrote", out)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c4", action="store_true")
+    ap.add_argument("--skip-small", action="store_true")
+    a = ap.parse_args()
+    if not a.skip_small:
+        small(os.path.join(HERE, "golden_small.npz"))
+    large(os.path.join(HERE, "golden_large.json"), a.c4)

@@ -1,0 +1,751 @@
+// vtk_api.cpp — C-ABI of libvtkrylov.so: contexts, RCCL communicator, CSR operator, block-Jacobi
+// preconditioner and the restarted GMRES driver (host orchestration of the gfx950 kernels).
+//
+// The driver restates scipy.sparse.linalg.gmres (scipy/sparse/linalg/_isolve/iterative.py:
+// 692-841) with every vector operation and every reduction on the device; the host only keeps
+// SciPy's outer-loop bookkeeping (ptol_max_factor, :816-838) and reads back one 100-byte state
+// record per restart cycle.  Inside a cycle the Givens rotations, the inner stop test
+// (presid <= ptol, :794) and the breakdown test (:766) run on the device: kernels of columns
+// after the stop column return at entry (GmresState::stop_col), so the host enqueues a cycle
+// without a per-step round trip and throttles itself with events LOOKAHEAD columns behind.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vtk_internal.hpp"
+#include "vtk_vlasov.hpp"
+
+namespace vtk {
+std::string context_free_error();
+bool vlasov_params_ok(const vtk_vlasov_params *p);
+}  // namespace vtk
+
+using namespace vtk;
+
+namespace {
+
+constexpr int LOOKAHEAD = 3;   // columns the host may run ahead of the device
+
+int fail(vtk_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    else set_context_free_error(msg);
+    return code;
+}
+
+#define HIPCHK(c, x)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess)                                                                \
+            return fail((c), e_ == hipErrorOutOfMemory ? VTK_ERR_NOMEM : VTK_ERR_HIP,        \
+                        std::string(#x) + ": " + hipGetErrorString(e_));                     \
+    } while (0)
+
+#define NCCLCHK(c, x)                                                                        \
+    do {                                                                                     \
+        ncclResult_t r_ = (x);                                                               \
+        if (r_ != ncclSuccess)                                                               \
+            return fail((c), VTK_ERR_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+#define TRY(x)                          \
+    do {                                \
+        int rc_ = (x);                  \
+        if (rc_ != VTK_OK) return rc_;  \
+    } while (0)
+
+// device buffer owned by a scope
+struct DBuf {
+    void *p = nullptr;
+    ~DBuf() { if (p) (void)hipFree(p); }
+    template <typename T> T *as() const { return static_cast<T *>(p); }
+};
+
+int dalloc(vtk_ctx *c, DBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    HIPCHK(c, hipMalloc(&b.p, bytes));
+    return VTK_OK;
+}
+
+int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tiles &t) {
+    std::vector<int32_t> rows;
+    build_tiles(indptr, align, rows, t.has_long, t.aligned);
+    t.ntiles = (int)rows.size() - 1;
+    t.align = align;
+    t.grid = std::max(1, std::min(t.ntiles, GMAX));
+    if (t.d_row) (void)hipFree(t.d_row);
+    t.d_row = nullptr;
+    HIPCHK(c, hipMalloc(&t.d_row, rows.size() * sizeof(int32_t)));
+    HIPCHK(c, hipMemcpy(t.d_row, rows.data(), rows.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    return VTK_OK;
+}
+
+// partial sums -> consumer view; across ranks: finalise to a scalar slot + RCCL all-reduce
+Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
+    rc = VTK_OK;
+    if (c->world == 1) return Red{part, cnt};
+    static thread_local int slot = 0;
+    double *dst = c->d_scal + (slot++ & 255);
+    hipError_t e = launch_finalize(Red{part, cnt}, dst, 0, c->stream);
+    if (e != hipSuccess) { rc = fail(c, VTK_ERR_HIP, hipGetErrorString(e)); return Red{dst, 1}; }
+    ncclResult_t r = ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) rc = fail(c, VTK_ERR_RCCL, ncclGetErrorString(r));
+    return Red{dst, 1};
+}
+
+int halo_exchange(vtk_csr *A, const double *x) {
+    vtk_ctx *c = A->ctx;
+    if (c->world == 1) return VTK_OK;
+    HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
+    NCCLCHK(c, ncclGroupStart());
+    for (int q = 0; q < c->world; ++q) {
+        if (A->send_cnt[q] > 0)
+            NCCLCHK(c, ncclSend(A->d_send_buf + A->send_off[q], (size_t)A->send_cnt[q], ncclDouble, q, c->comm, c->stream));
+        if (A->recv_cnt[q] > 0)
+            NCCLCHK(c, ncclRecv(A->d_halo + A->recv_off[q], (size_t)A->recv_cnt[q], ncclDouble, q, c->comm, c->stream));
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    return VTK_OK;
+}
+
+SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x) {
+    return SpmvIn{A->d_indptr, A->d_indices, A->d_data, A->fp32, t, (int)A->n_local, x,
+                  A->ctx->world > 1 ? A->d_halo : nullptr};
+}
+
+// Build the halo plan of a freshly uploaded CSR (indices still GLOBAL on the device), remap
+// the device indices to local numbering and exchange the send lists over RCCL.
+int setup_halo(vtk_csr *A) {
+    vtk_ctx *c = A->ctx;
+    const int W = c->world;
+    std::vector<int32_t> idx((size_t)A->nnz);
+    if (A->nnz) HIPCHK(c, hipMemcpy(idx.data(), A->d_indices, A->nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    int64_t nh = 0;
+    if (vtk_halo_plan(A->n_global, A->offsets.data(), W, c->rank, A->nnz, idx.data(), nullptr, &nh,
+                      nullptr, nullptr) != VTK_OK)
+        return fail(c, VTK_ERR_ARG, context_free_error());
+    A->halo_cols.resize((size_t)nh);
+    A->recv_cnt.assign(W, 0);
+    if (vtk_halo_plan(A->n_global, A->offsets.data(), W, c->rank, A->nnz, idx.data(), nullptr, &nh,
+                      A->halo_cols.data(), A->recv_cnt.data()) != VTK_OK)
+        return fail(c, VTK_ERR_ARG, context_free_error());
+    A->n_halo = nh;
+    A->recv_off.assign(W, 0);
+    for (int q = 1; q < W; ++q) A->recv_off[q] = A->recv_off[q - 1] + A->recv_cnt[q - 1];
+    // remap indices on the device
+    DBuf dh;
+    TRY(dalloc(c, dh, (size_t)nh * sizeof(int64_t)));
+    if (nh) HIPCHK(c, hipMemcpy(dh.p, A->halo_cols.data(), nh * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(c, launch_remap_cols(A->d_indices, A->nnz, A->row_begin, A->n_local, dh.as<int64_t>(), nh, c->stream));
+    // counts matrix: everyone learns what it must send
+    DBuf dcnt, dall;
+    TRY(dalloc(c, dcnt, W * sizeof(int64_t)));
+    TRY(dalloc(c, dall, (size_t)W * W * sizeof(int64_t)));
+    HIPCHK(c, hipMemcpyAsync(dcnt.p, A->recv_cnt.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(c, ncclAllGather(dcnt.p, dall.p, W, ncclInt64, c->comm, c->stream));
+    std::vector<int64_t> all((size_t)W * W);
+    HIPCHK(c, hipMemcpyAsync(all.data(), dall.p, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    A->send_cnt.assign(W, 0);
+    A->send_off.assign(W, 0);
+    for (int q = 0; q < W; ++q) A->send_cnt[q] = all[(size_t)q * W + c->rank];
+    for (int q = 1; q < W; ++q) A->send_off[q] = A->send_off[q - 1] + A->send_cnt[q - 1];
+    A->n_send = W ? A->send_off[W - 1] + A->send_cnt[W - 1] : 0;
+    // exchange the requested global ids
+    DBuf dreq, dsend;
+    TRY(dalloc(c, dreq, (size_t)nh * sizeof(int64_t)));
+    TRY(dalloc(c, dsend, (size_t)A->n_send * sizeof(int64_t)));
+    if (nh) HIPCHK(c, hipMemcpyAsync(dreq.p, A->halo_cols.data(), nh * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(c, ncclGroupStart());
+    for (int q = 0; q < W; ++q) {
+        if (A->recv_cnt[q] > 0)
+            NCCLCHK(c, ncclSend(dreq.as<int64_t>() + A->recv_off[q], (size_t)A->recv_cnt[q], ncclInt64, q, c->comm, c->stream));
+        if (A->send_cnt[q] > 0)
+            NCCLCHK(c, ncclRecv(dsend.as<int64_t>() + A->send_off[q], (size_t)A->send_cnt[q], ncclInt64, q, c->comm, c->stream));
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    std::vector<int64_t> sg((size_t)A->n_send);
+    if (A->n_send) HIPCHK(c, hipMemcpyAsync(sg.data(), dsend.p, A->n_send * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<int32_t> sl((size_t)A->n_send);
+    for (int64_t k = 0; k < A->n_send; ++k) {
+        const int64_t l = sg[k] - A->row_begin;
+        if (l < 0 || l >= A->n_local) return fail(c, VTK_ERR_STATE, "halo request for a row this rank does not own");
+        sl[k] = (int32_t)l;
+    }
+    HIPCHK(c, hipMalloc(&A->d_send_idx, std::max<int64_t>(1, A->n_send) * sizeof(int32_t)));
+    HIPCHK(c, hipMalloc(&A->d_send_buf, std::max<int64_t>(1, A->n_send) * sizeof(double)));
+    HIPCHK(c, hipMalloc(&A->d_halo, std::max<int64_t>(1, nh) * sizeof(double)));
+    if (A->n_send) HIPCHK(c, hipMemcpy(A->d_send_idx, sl.data(), A->n_send * sizeof(int32_t), hipMemcpyHostToDevice));
+    return VTK_OK;
+}
+
+int finish_csr(vtk_csr *A) {
+    vtk_ctx *c = A->ctx;
+    if (c->world > 1) TRY(setup_halo(A));
+    TRY(upload_tiles(c, A->h_indptr, 1, A->tiles));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VTK_OK;
+}
+
+int check_partition(vtk_ctx *c, int64_t n_global, const int64_t *offsets, std::vector<int64_t> &out) {
+    out.resize(c->world + 1);
+    if (c->world == 1) {
+        out[0] = 0;
+        out[1] = n_global;
+        if (offsets && (offsets[0] != 0 || offsets[1] != n_global)) return fail(c, VTK_ERR_ARG, "offsets must be {0, n}");
+        return VTK_OK;
+    }
+    if (!offsets) return fail(c, VTK_ERR_ARG, "offsets required when world > 1");
+    for (int q = 0; q <= c->world; ++q) out[q] = offsets[q];
+    if (out[0] != 0 || out[c->world] != n_global) return fail(c, VTK_ERR_ARG, "offsets must span [0, n)");
+    for (int q = 0; q < c->world; ++q)
+        if (out[q + 1] < out[q]) return fail(c, VTK_ERR_ARG, "offsets must be non-decreasing");
+    return VTK_OK;
+}
+
+void destroy_csr(vtk_csr *A) {
+    if (!A) return;
+    if (A->ctx) (void)hipSetDevice(A->ctx->device);
+    (void)hipFree(A->d_indptr);
+    (void)hipFree(A->d_indices);
+    (void)hipFree(A->d_data);
+    (void)hipFree(A->tiles.d_row);
+    (void)hipFree(A->d_halo);
+    (void)hipFree(A->d_send_idx);
+    (void)hipFree(A->d_send_buf);
+    delete A;
+}
+
+// ---- GMRES -----------------------------------------------------------------------------------
+
+struct Solver {
+    vtk_csr *A;
+    vtk_prec *M;
+    vtk_ctx *c;
+    int64_t n, ld;
+    int m, G;
+    double *V, *w, *tmp, *r, *H, *S, *giv;
+    double *part[4];
+};
+
+// w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
+int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0) {
+    vtk_ctx *c = s.c;
+    vtk_csr *A = s.A;
+    TRY(halo_exchange(A, v));
+    const double *v0 = s.V;
+    int cnt;
+    if (!s.M) {
+        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PREC, w, nullptr, nullptr, 0, v0, s.part[0], s.part[1], stop, col, c->stream));
+        cnt = A->tiles.grid;
+    } else if (s.M->fused) {
+        HIPCHK(c, launch_spmv(spmv_in(A, &s.M->tiles, v), EPI_PREC, w, nullptr, s.M->d_inv, s.M->bs, v0, s.part[0], s.part[1], stop, col, c->stream));
+        cnt = s.M->tiles.grid;
+    } else {
+        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, nullptr, 0, nullptr, nullptr, nullptr, stop, col, c->stream));
+        HIPCHK(c, launch_bj_apply(s.M->d_inv, s.M->bs, s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
+        cnt = s.G;
+    }
+    int rc;
+    h0 = reduce(c, s.part[0], cnt, rc);
+    TRY(rc);
+    d0 = reduce(c, s.part[1], cnt, rc);
+    return rc;
+}
+
+int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, double atol,
+              int restart, int64_t maxiter, int *info, vtk_stats *stout) {
+    vtk_ctx *c = A->ctx;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t n = A->n_local, N = A->n_global;
+    if (maxiter <= 0) maxiter = N * 10;                     // iterative.py:726-727
+    if (restart <= 0) restart = 20;                         // :729-730
+    if (restart > N) restart = (int)N;                      // :731
+    if (restart > MAX_RESTART) return fail(c, VTK_ERR_ARG, "restart exceeds MAX_RESTART");
+    if (restart < 1) return fail(c, VTK_ERR_ARG, "empty system");
+    const int m = restart;
+    Solver s{A, M, c, n, round_up(std::max<int64_t>(n, 1), 64), m, vector_grid(n), nullptr, nullptr,
+             nullptr, nullptr, nullptr, nullptr, nullptr, {c->d_part, c->d_part + GMAX, c->d_part + 2 * GMAX, c->d_part + 3 * GMAX}};
+    // workspace: V[(m+1) x ld] | w | tmp | r | H[m x (m+1)] | S[m+1] | giv[2m]  (doubles)
+    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64;
+    if (c->ws_bytes < nd * sizeof(double)) {
+        if (c->ws) (void)hipFree(c->ws);
+        c->ws = nullptr;
+        c->ws_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->ws, nd * sizeof(double)));
+        c->ws_bytes = nd * sizeof(double);
+    }
+    double *wp = static_cast<double *>(c->ws);
+    s.V = wp; wp += (size_t)(m + 1) * s.ld;
+    s.w = wp; wp += s.ld;
+    s.tmp = wp; wp += s.ld;
+    s.r = wp; wp += s.ld;
+    s.H = wp; wp += (size_t)m * (m + 1);
+    s.S = wp; wp += m + 1;
+    s.giv = wp;
+    HIPCHK(c, hipMemsetAsync(s.H, 0, (size_t)m * (m + 1) * sizeof(double), c->stream));
+    HIPCHK(c, hipMemsetAsync(s.giv, 0, (size_t)2 * m * sizeof(double), c->stream));
+    GmresState *ds = c->d_state, *hs = c->h_state;
+    std::memset(hs, 0, sizeof(GmresState));
+    hs->stop_col = BIG_COL;
+    HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(GmresState), hipMemcpyHostToDevice, c->stream));
+    int rc;
+    // ||b|| and ||M b|| (iterative.py:708, :714)
+    HIPCHK(c, launch_dot(b, nullptr, n, s.part[0], s.G, c->stream));
+    Red rb = reduce(c, s.part[0], s.G, rc);
+    TRY(rc);
+    HIPCHK(c, launch_finalize(rb, &ds->scal[0], 1, c->stream));
+    HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream));
+    Red rmb = reduce(c, s.part[1], s.G, rc);
+    TRY(rc);
+    HIPCHK(c, launch_finalize(rmb, &ds->scal[1], 1, c->stream));
+    // r = b - A x (iterative.py:737)
+    TRY(halo_exchange(A, x));
+    HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream));
+    Red rr = reduce(c, s.part[2], A->tiles.grid, rc);
+    TRY(rc);
+    HIPCHK(c, launch_finalize(rr, &ds->rnorm, 1, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const double bnrm2 = hs->scal[0], Mb_nrm2 = hs->scal[1];
+    const double eps = 2.220446049250313e-16;
+    atol = std::max(atol, rtol * bnrm2);                    // _get_atol_rtol :19
+    vtk_stats st{};
+    st.bnorm = bnrm2;
+    st.atol_eff = atol;
+    st.orth = VTK_ORTH_MGS;
+    auto done = [&](int inf) {
+        *info = inf;
+        st.t_solve = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (stout) *stout = st;
+        return VTK_OK;
+    };
+    if (bnrm2 == 0.0) {                                     // :712-713 -> x = b
+        HIPCHK(c, hipMemcpyAsync(x, b, n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return done(0);
+    }
+    double rnorm = hs->rnorm;
+    if (rnorm < atol) { st.rnorm = rnorm; return done(0); }   // :738-739
+    double ptol_max_factor = 1.0;
+    double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);   // :723
+    double presid = 0.0;
+    const double bytes_spmv = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 16.0 * n;
+    const double bytes_pc = M ? (8.0 * M->bs * n + 16.0 * n) : 16.0 * n;
+    hipEvent_t ev[LOOKAHEAD + 1];
+    for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    struct EvGuard { hipEvent_t *e; ~EvGuard() { for (int i = 0; i <= LOOKAHEAD; ++i) (void)hipEventDestroy(e[i]); } } eg{ev};
+    volatile int *mirror = c->h_stop;
+    int64_t it = 0;
+    bool brk = false;
+    for (it = 0; it < maxiter; ++it) {
+        // cycle start: v0 = M^-1 r / ||M^-1 r||, S = [tmp, 0, ...] (:742-748)
+        hs->ptol = ptol;
+        HIPCHK(c, hipMemcpyAsync(&ds->ptol, &hs->ptol, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream));
+        Red rv = reduce(c, s.part[0], s.G, rc);
+        TRY(rc);
+        HIPCHK(c, launch_scale0(rv, s.V, n, s.S, m, ds, s.G, c->stream));
+        const int *stop = &ds->stop_col;
+        *mirror = BIG_COL;
+        int enq = 0;
+        for (int col = 0; col < m; ++col) {
+            double *vcol = s.V + (size_t)col * s.ld;
+            Red h0, d0;
+            TRY(precond_matvec(s, vcol, s.w, stop, col, h0, d0));
+            Red cur = d0;
+            for (int k = 0; k <= col; ++k) {
+                double *po = s.part[2 + (k & 1)];
+                const double *vn = k < col ? s.V + (size_t)(k + 1) * s.ld : nullptr;
+                HIPCHK(c, launch_mgs(cur, s.H + (size_t)col * (m + 1) + k, s.w, s.V + (size_t)k * s.ld, vn, n, po, s.G, stop, col, c->stream));
+                cur = reduce(c, po, s.G, rc);
+                TRY(rc);
+            }
+            HIPCHK(c, launch_tail(h0, cur, s.w, s.V + (size_t)(col + 1) * s.ld, n, col, m, s.H, s.S, s.giv, ds, c->d_stop, s.G, c->stream));
+            HIPCHK(c, hipEventRecord(ev[col % (LOOKAHEAD + 1)], c->stream));
+            enq = col + 1;
+            if (col >= LOOKAHEAD) {
+                HIPCHK(c, hipEventSynchronize(ev[(col - LOOKAHEAD) % (LOOKAHEAD + 1)]));
+                if (*mirror < BIG_COL) break;   // stopped: no further columns needed
+            }
+        }
+        (void)enq;
+        // x += y @ V[:col+1] (:799-814), r = b - A x, rnorm (:816-817)
+        HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream));
+        TRY(halo_exchange(A, x));
+        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream));
+        Red rr2 = reduce(c, s.part[2], A->tiles.grid, rc);
+        TRY(rc);
+        HIPCHK(c, launch_finalize(rr2, &ds->rnorm, 1, c->stream));
+        HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const int last = hs->stop_col < m ? hs->stop_col : m - 1;
+        for (int j = 0; j <= last; ++j) st.bytes_moved += bytes_spmv + bytes_pc + 8.0 * n * (2 * j + 8);
+        st.bytes_moved += bytes_spmv + 24.0 * n + bytes_pc + 24.0 * n + 8.0 * n * (last + 2);
+        rnorm = hs->rnorm;
+        presid = hs->presid;
+        brk = hs->breakdown != 0;
+        st.restarts = it + 1;
+        if (rnorm <= atol) break;                                                   // :824
+        else if (brk) break;                                                        // :826
+        else if (presid <= ptol) ptol_max_factor = std::max(eps, 0.25 * ptol_max_factor);   // :830
+        else ptol_max_factor = std::min(1.0, 1.5 * ptol_max_factor);              // :833
+        ptol = presid * std::min(ptol_max_factor, atol / rnorm);                    // :835
+    }
+    st.inner_iters = hs->inner;
+    st.presid = presid;
+    st.rnorm = rnorm;
+    st.breakdown = brk ? 1 : 0;
+    return done(rnorm <= atol ? 0 : (int)std::min<int64_t>(maxiter, INT32_MAX));   // :840
+}
+
+}  // namespace
+
+extern "C" {
+
+int vtk_last_error(vtk_ctx *ctx, char *buf, size_t len) {
+    if (!buf || len == 0) return VTK_ERR_ARG;
+    const std::string e = ctx ? ctx->err : context_free_error();
+    std::snprintf(buf, len, "%s", e.c_str());
+    return VTK_OK;
+}
+
+int vtk_device_count(int *count) {
+    if (!count) return VTK_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return VTK_OK;
+}
+
+int vtk_ctx_create(int device, vtk_ctx **out) {
+    if (!out) return fail(nullptr, VTK_ERR_ARG, "vtk_ctx_create: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(nullptr, VTK_ERR_NODEVICE, "vtk_ctx_create: no HIP device visible (the product has no CPU fallback)");
+    if (device < 0 || device >= n) return fail(nullptr, VTK_ERR_ARG, "vtk_ctx_create: bad device ordinal");
+    auto *c = new vtk_ctx();
+    c->device = device;
+    auto bad = [&](hipError_t e) {
+        set_context_free_error(std::string("vtk_ctx_create: ") + hipGetErrorString(e));
+        vtk_ctx_destroy(c);
+        return e == hipErrorOutOfMemory ? VTK_ERR_NOMEM : VTK_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return bad(e);
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e);
+    if ((e = hipMalloc(&c->d_part, 8 * GMAX * sizeof(double))) != hipSuccess) return bad(e);
+    if ((e = hipMalloc(&c->d_scal, 256 * sizeof(double))) != hipSuccess) return bad(e);
+    if ((e = hipMalloc(&c->d_state, sizeof(GmresState))) != hipSuccess) return bad(e);
+    if ((e = hipHostMalloc(&c->h_state, sizeof(GmresState), hipHostMallocDefault)) != hipSuccess) return bad(e);
+    if ((e = hipHostMalloc(&c->h_stop, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess) return bad(e);
+    if ((e = hipHostGetDevicePointer((void **)&c->d_stop, c->h_stop, 0)) != hipSuccess) return bad(e);
+    *c->h_stop = BIG_COL;
+    *out = c;
+    return VTK_OK;
+}
+
+void vtk_ctx_destroy(vtk_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_part);
+    (void)hipFree(c->d_scal);
+    (void)hipFree(c->d_state);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_stop) (void)hipHostFree(c->h_stop);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int vtk_ctx_stream(vtk_ctx *c, void **stream) {
+    if (!c || !stream) return VTK_ERR_ARG;
+    *stream = (void *)c->stream;
+    return VTK_OK;
+}
+
+int vtk_ctx_synchronize(vtk_ctx *c) {
+    if (!c) return VTK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VTK_OK;
+}
+
+int vtk_comm_unique_id(void *out128) {
+    if (!out128) return fail(nullptr, VTK_ERR_ARG, "vtk_comm_unique_id: NULL");
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, VTK_ERR_RCCL, ncclGetErrorString(r));
+    std::memcpy(out128, &id, sizeof(id));
+    return VTK_OK;
+}
+
+int vtk_comm_init(vtk_ctx *c, int rank, int world, const void *uid) {
+    if (!c || world < 1 || rank < 0 || rank >= world) return fail(c, VTK_ERR_ARG, "vtk_comm_init: bad rank/world");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (world == 1) { c->rank = 0; c->world = 1; return VTK_OK; }
+    if (!uid) return fail(c, VTK_ERR_ARG, "vtk_comm_init: unique id required");
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
+    c->rank = rank;
+    c->world = world;
+    return VTK_OK;
+}
+
+int vtk_comm_info(vtk_ctx *c, int *rank, int *world) {
+    if (!c || !rank || !world) return VTK_ERR_ARG;
+    *rank = c->rank;
+    *world = c->world;
+    return VTK_OK;
+}
+
+int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t nnz,
+                   const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
+                   int kind, vtk_csr **out) {
+    if (!c || !out || n_global < 0 || nnz < 0 || !indptr || (nnz > 0 && (!indices || !data)))
+        return fail(c, VTK_ERR_ARG, "vtk_csr_create: invalid arguments");
+    if (nnz >= ((int64_t)1 << 31)) return fail(c, VTK_ERR_ARG, "vtk_csr_create: nnz must fit int32");
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<int64_t> offs;
+    TRY(check_partition(c, n_global, offsets, offs));
+    auto *A = new vtk_csr();
+    struct Guard { vtk_csr *&a; ~Guard() { if (a) destroy_csr(a); } } g{A};
+    A->ctx = c;
+    A->n_global = n_global;
+    A->offsets = offs;
+    A->row_begin = offs[c->rank];
+    A->row_end = offs[c->rank + 1];
+    A->n_local = A->row_end - A->row_begin;
+    A->nnz = nnz;
+    A->fp32 = fp32 ? 1 : 0;
+    const int64_t nl = A->n_local;
+    A->h_indptr.resize(nl + 1);
+    const hipMemcpyKind k = kind == VTK_PTR_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost;
+    HIPCHK(c, hipMemcpy(A->h_indptr.data(), indptr, (nl + 1) * sizeof(int32_t), k));
+    if (A->h_indptr[0] != 0 || A->h_indptr[nl] != nnz) return fail(c, VTK_ERR_ARG, "vtk_csr_create: indptr must start at 0 and end at nnz");
+    for (int64_t i = 0; i < nl; ++i)
+        if (A->h_indptr[i + 1] < A->h_indptr[i]) return fail(c, VTK_ERR_ARG, "vtk_csr_create: indptr not monotone");
+    if (kind == VTK_PTR_HOST) {
+        for (int64_t kk = 0; kk < nnz; ++kk)
+            if (indices[kk] < 0 || indices[kk] >= n_global) return fail(c, VTK_ERR_ARG, "vtk_csr_create: column index out of range");
+    }
+    const size_t vb = fp32 ? sizeof(float) : sizeof(double);
+    HIPCHK(c, hipMalloc(&A->d_indptr, (nl + 1) * sizeof(int32_t)));
+    HIPCHK(c, hipMalloc(&A->d_indices, std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
+    HIPCHK(c, hipMalloc(&A->d_data, std::max<int64_t>(nnz, 1) * vb));
+    const hipMemcpyKind kd = kind == VTK_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    HIPCHK(c, hipMemcpy(A->d_indptr, A->h_indptr.data(), (nl + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (nnz) {
+        HIPCHK(c, hipMemcpy(A->d_indices, indices, nnz * sizeof(int32_t), kd));
+        HIPCHK(c, hipMemcpy(A->d_data, data, nnz * vb, kd));
+    }
+    TRY(finish_csr(A));
+    *out = A;
+    A = nullptr;
+    return VTK_OK;
+}
+
+int vtk_csr_create_vlasov(vtk_ctx *c, const vtk_vlasov_params *p, const int64_t *offsets, vtk_csr **out) {
+    if (!c || !out || !vlasov_params_ok(p)) return fail(c, VTK_ERR_ARG, "vtk_csr_create_vlasov: invalid arguments");
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t N = vlasov_n(*p);
+    if (vlasov_nnz(*p) >= ((int64_t)1 << 31)) return fail(c, VTK_ERR_ARG, "vtk_csr_create_vlasov: nnz must fit int32");
+    std::vector<int64_t> offs;
+    TRY(check_partition(c, N, offsets, offs));
+    auto *A = new vtk_csr();
+    struct Guard { vtk_csr *&a; ~Guard() { if (a) destroy_csr(a); } } g{A};
+    A->ctx = c;
+    A->n_global = N;
+    A->offsets = offs;
+    A->row_begin = offs[c->rank];
+    A->row_end = offs[c->rank + 1];
+    A->n_local = A->row_end - A->row_begin;
+    A->fp32 = p->fp32 ? 1 : 0;
+    const int64_t nl = A->n_local;
+    HIPCHK(c, hipMalloc(&A->d_indptr, (nl + 1) * sizeof(int32_t)));
+    HIPCHK(c, launch_vlasov_counts(*p, A->row_begin, nl, A->d_indptr, c->stream));
+    size_t tb = 0;
+    HIPCHK(c, launch_exclusive_scan(nullptr, nullptr, nl + 1, nullptr, &tb, c->stream));
+    DBuf tmp, cnt;
+    TRY(dalloc(c, tmp, tb));
+    TRY(dalloc(c, cnt, (nl + 1) * sizeof(int32_t)));
+    HIPCHK(c, hipMemcpyAsync(cnt.p, A->d_indptr, (nl + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, launch_exclusive_scan(cnt.as<int32_t>(), A->d_indptr, nl + 1, tmp.p, &tb, c->stream));
+    A->h_indptr.resize(nl + 1);
+    HIPCHK(c, hipMemcpyAsync(A->h_indptr.data(), A->d_indptr, (nl + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    A->nnz = A->h_indptr[nl];
+    const size_t vb = A->fp32 ? sizeof(float) : sizeof(double);
+    HIPCHK(c, hipMalloc(&A->d_indices, std::max<int64_t>(A->nnz, 1) * sizeof(int32_t)));
+    HIPCHK(c, hipMalloc(&A->d_data, std::max<int64_t>(A->nnz, 1) * vb));
+    HIPCHK(c, launch_vlasov_fill(*p, A->row_begin, nl, A->d_indptr, A->d_indices, A->d_data, c->stream));
+    TRY(finish_csr(A));
+    *out = A;
+    A = nullptr;
+    return VTK_OK;
+}
+
+int vtk_csr_info(vtk_csr *A, int64_t *n_global, int64_t *row_begin, int64_t *row_end, int64_t *nnz, int64_t *n_halo) {
+    if (!A) return VTK_ERR_ARG;
+    if (n_global) *n_global = A->n_global;
+    if (row_begin) *row_begin = A->row_begin;
+    if (row_end) *row_end = A->row_end;
+    if (nnz) *nnz = A->nnz;
+    if (n_halo) *n_halo = A->n_halo;
+    return VTK_OK;
+}
+
+int vtk_csr_download(vtk_csr *A, int32_t *indptr, int32_t *indices, void *data) {
+    if (!A || !indptr || (A->nnz && (!indices || !data))) return VTK_ERR_ARG;
+    vtk_ctx *c = A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memcpy(indptr, A->h_indptr.data(), A->h_indptr.size() * sizeof(int32_t));
+    if (!A->nnz) return VTK_OK;
+    HIPCHK(c, hipMemcpy(indices, A->d_indices, A->nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(data, A->d_data, A->nnz * (A->fp32 ? sizeof(float) : sizeof(double)), hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < A->nnz; ++k) {
+        const int64_t l = indices[k];
+        indices[k] = (int32_t)(l < A->n_local ? l + A->row_begin : A->halo_cols[l - A->n_local]);
+    }
+    return VTK_OK;
+}
+
+void vtk_csr_destroy(vtk_csr *A) { destroy_csr(A); }
+
+// host <-> device staging for the *_HOST forms
+struct Staged {
+    vtk_ctx *c;
+    DBuf buf;
+    double *d = nullptr;
+};
+
+static int stage_in(vtk_ctx *c, const double *src, int64_t n, int kind, Staged &s) {
+    s.c = c;
+    if (kind == VTK_PTR_DEVICE) { s.d = const_cast<double *>(src); return VTK_OK; }
+    TRY(dalloc(c, s.buf, std::max<int64_t>(n, 1) * sizeof(double)));
+    s.d = s.buf.as<double>();
+    if (n && src) HIPCHK(c, hipMemcpyAsync(s.d, src, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return VTK_OK;
+}
+
+int vtk_spmv(vtk_csr *A, const double *x, double *y, int kind) {
+    if (!A || !x || !y) return VTK_ERR_ARG;
+    vtk_ctx *c = A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    Staged sx, sy;
+    TRY(stage_in(c, x, A->n_local, kind, sx));
+    TRY(stage_in(c, kind == VTK_PTR_DEVICE ? y : nullptr, A->n_local, kind, sy));
+    TRY(halo_exchange(A, sx.d));
+    HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, sx.d), EPI_PLAIN, sy.d, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, c->stream));
+    if (kind == VTK_PTR_HOST) {
+        HIPCHK(c, hipMemcpyAsync(y, sy.d, A->n_local * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return VTK_OK;
+}
+
+int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
+    if (!A || !out || bs < 1 || bs > 64) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_bjacobi_create: block size must be in [1, 64]");
+    vtk_ctx *c = A->ctx;
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (A->row_begin % bs != 0) return fail(c, VTK_ERR_ARG, "vtk_bjacobi_create: rank row block must start at a multiple of the block size");
+    auto *M = new vtk_prec();
+    struct Guard { vtk_prec *&m; ~Guard() { if (m) vtk_prec_destroy(m); } } g{M};
+    M->A = A;
+    M->bs = bs;
+    M->nb = (A->n_local + bs - 1) / bs;
+    HIPCHK(c, hipMalloc(&M->d_inv, std::max<int64_t>(M->nb, 1) * bs * bs * sizeof(double)));
+    DBuf sing, work;
+    TRY(dalloc(c, sing, sizeof(int)));
+    const bool pow2 = (bs & (bs - 1)) == 0 && bs <= 32;
+    if (!pow2) TRY(dalloc(c, work, std::max<int64_t>(M->nb, 1) * bs * bs * sizeof(double)));
+    const int init = INT32_MAX;
+    HIPCHK(c, hipMemcpyAsync(sing.p, &init, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_bj_setup(A->d_indptr, A->d_indices, A->d_data, A->fp32, A->n_local, bs, M->d_inv, sing.as<int>(), work.as<double>(), c->stream));
+    int sb = 0;
+    HIPCHK(c, hipMemcpyAsync(&sb, sing.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (sb != INT32_MAX) return fail(c, VTK_ERR_SINGULAR, "vtk_bjacobi_create: singular diagonal block " + std::to_string(sb + A->row_begin / bs));
+    if (pow2) {
+        TRY(upload_tiles(c, A->h_indptr, bs, M->tiles));
+        M->fused = M->tiles.aligned && !M->tiles.has_long;
+    }
+    *out = M;
+    M = nullptr;
+    return VTK_OK;
+}
+
+int vtk_bjacobi_inverse(vtk_prec *M, double *inv, int kind) {
+    if (!M || !inv) return VTK_ERR_ARG;
+    vtk_ctx *c = M->A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(inv, M->d_inv, M->nb * M->bs * M->bs * sizeof(double), kind == VTK_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    return VTK_OK;
+}
+
+int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
+    if (!M || !r || !z) return VTK_ERR_ARG;
+    vtk_ctx *c = M->A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = M->A->n_local;
+    Staged sr, sz;
+    TRY(stage_in(c, r, n, kind, sr));
+    TRY(stage_in(c, kind == VTK_PTR_DEVICE ? z : nullptr, n, kind, sz));
+    HIPCHK(c, launch_bj_apply(M->d_inv, M->bs, n, sr.d, sz.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0, c->stream));
+    if (kind == VTK_PTR_HOST) {
+        HIPCHK(c, hipMemcpyAsync(z, sz.d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return VTK_OK;
+}
+
+void vtk_prec_destroy(vtk_prec *M) {
+    if (!M) return;
+    if (M->A && M->A->ctx) (void)hipSetDevice(M->A->ctx->device);
+    (void)hipFree(M->d_inv);
+    (void)hipFree(M->tiles.d_row);
+    delete M;
+}
+
+int vtk_gmres_set_orth(vtk_ctx *c, int orth) {
+    if (!c || (orth != VTK_ORTH_MGS && orth != VTK_ORTH_CGS2)) return VTK_ERR_ARG;
+    if (orth == VTK_ORTH_CGS2) return fail(c, VTK_ERR_ARG, "CGS2 not available in this build");
+    c->orth = orth;
+    return VTK_OK;
+}
+
+int vtk_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, double atol,
+              int restart, int64_t maxiter, int kind, int *info, vtk_stats *st) {
+    if (!A || !b || !x || !info) return VTK_ERR_ARG;
+    vtk_ctx *c = A->ctx;
+    if (M && M->A != A) return fail(c, VTK_ERR_ARG, "vtk_gmres: preconditioner built for another operator");
+    if (!(rtol >= 0.0) || !(atol >= 0.0)) return fail(c, VTK_ERR_ARG, "vtk_gmres: tolerances must be non-negative");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = A->n_local;
+    Staged sb, sx;
+    TRY(stage_in(c, b, n, kind, sb));
+    TRY(stage_in(c, x, n, kind, sx));
+    TRY(run_gmres(A, M, sb.d, sx.d, rtol, atol, restart, maxiter, info, st));
+    if (kind == VTK_PTR_HOST) {
+        HIPCHK(c, hipMemcpyAsync(x, sx.d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VTK_OK;
+}
+
+}  // extern "C"

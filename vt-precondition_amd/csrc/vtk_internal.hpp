@@ -1,0 +1,167 @@
+// vtk_internal.hpp — types shared by the C-ABI/driver (vtk_api.cpp, vtk_host.cpp) and the
+// gfx950 kernels (vtk_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/vtkrylov.h"
+
+namespace vtk {
+
+// ---- kernel geometry -------------------------------------------------------
+constexpr int NT = 256;            // threads per workgroup, every vector kernel
+constexpr int TILE_ROWS = 512;     // max rows of one SpMV tile (CSR-stream)
+constexpr int TILE_NNZ = 4096;     // max nnz of one stream tile: products staged in LDS (32 KB)
+constexpr int GMAX = 1024;         // max workgroups of a reducing kernel = partial-sum slots
+constexpr int MAX_RESTART = 1024;  // restart length bound (LDS for y in the x update)
+constexpr int BIG_COL = 1 << 30;   // "not stopped" marker of GmresState::stop_col
+
+// ---- device-resident solver scalars ---------------------------------------------------------
+struct GmresState {
+    double ptol;          // inner tolerance of this cycle (host writes before each cycle)
+    double presid;        // |S[col+1]| after the last Givens step
+    double rnorm;         // ||b - A x|| (finalise)
+    double scal[8];       // misc finalised scalars (bnorm, Mb norm, ...)
+    int stop_col;         // column at which the cycle stopped (BIG_COL while running)
+    int breakdown;        // h1 <= eps*h0 at stop_col
+    long long inner;      // inner iterations, cumulative
+};
+
+// a reduced scalar as seen by a consumer kernel: G partials (single GPU) or 1 value (after
+// the RCCL all-reduce).  Every consumer workgroup sums the partials in the same fixed order.
+struct Red {
+    const double *p;
+    int cnt;
+};
+
+// ---- CSR tiles (CSR-stream row blocks) -----------------------------------------------------
+struct Tiles {
+    int32_t *d_row = nullptr;   // tile t = rows [row[t], row[t+1])
+    int ntiles = 0;
+    int align = 1;              // every boundary is a multiple of align (except n_local)
+    bool has_long = false;      // some tile is a single row with nnz > TILE_NNZ
+    bool aligned = true;        // no align-group had to be split into single-row tiles
+    int grid = 0;               // workgroups of the tile kernels = min(ntiles, GMAX)
+};
+
+}  // namespace vtk
+
+struct vtk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+    int orth = VTK_ORTH_MGS;
+    // scratch shared by calls on this context
+    double *d_part = nullptr;        // [8][GMAX] partial sums
+    double *d_scal = nullptr;        // [256] reduced scalars (all-reduce slots)
+    vtk::GmresState *d_state = nullptr;
+    vtk::GmresState *h_state = nullptr;   // pinned mirror
+    int *h_stop = nullptr;                // pinned, device-mapped: k_tail writes the stop column
+    int *d_stop = nullptr;                // device alias of h_stop
+    void *ws = nullptr;                   // solver workspace (grow-only, reused across solves)
+    size_t ws_bytes = 0;
+};
+
+struct vtk_csr {
+    vtk_ctx *ctx = nullptr;
+    int64_t n_global = 0, row_begin = 0, row_end = 0, n_local = 0, nnz = 0;
+    int fp32 = 0;
+    int32_t *d_indptr = nullptr, *d_indices = nullptr;  // local column indices
+    void *d_data = nullptr;
+    std::vector<int32_t> h_indptr;                      // host copy (tile planning)
+    std::vector<int64_t> offsets;                       // partition, world+1
+    vtk::Tiles tiles;                                   // align 1
+    // halo (world > 1)
+    int64_t n_halo = 0;
+    std::vector<int64_t> halo_cols;                     // global ids, ascending
+    std::vector<int64_t> recv_cnt, recv_off;            // per rank, into d_halo
+    std::vector<int64_t> send_cnt, send_off;            // per rank, into d_send_buf
+    double *d_halo = nullptr;
+    int32_t *d_send_idx = nullptr;                      // local rows to pack
+    double *d_send_buf = nullptr;
+    int64_t n_send = 0;
+};
+
+struct vtk_prec {
+    vtk_csr *A = nullptr;
+    int bs = 8;
+    int64_t nb = 0;
+    double *d_inv = nullptr;     // [nb][bs][bs]
+    vtk::Tiles tiles;            // aligned to bs (fused SpMV + BJ)
+    bool fused = false;          // fused SpMV+BJ kernel usable
+};
+
+namespace vtk {
+
+// ---- kernel launchers (vtk_kernels.hip) ------------------------------------------------------
+struct SpmvIn {
+    const int32_t *indptr, *indices;
+    const void *data;
+    int fp32;
+    const Tiles *tiles;
+    int n_local;
+    const double *x, *halo;   // halo may be null (world == 1)
+};
+
+enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2 };
+
+// y = A x (PLAIN); y = b - A x, part0 = sum y^2 (RESID); y = M^-1 A x with M = BJ(inv, bs)
+// or identity (inv == null), part0 = sum y^2, part1 = sum v0*y (PREC, v0 may be null).
+hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
+                       int bs, const double *v0, double *part0, double *part1,
+                       const int *stop_col, int col, hipStream_t s);
+// z = M^-1 r (BJ or identity when inv == null); part0 = sum z^2, part1 = sum v0*z (optional)
+hipError_t launch_bj_apply(const double *inv, int bs, int64_t n, const double *r, double *z,
+                           const double *v0, double *part0, double *part1, int grid,
+                           const int *stop_col, int col, hipStream_t s);
+hipError_t launch_bj_setup(const int32_t *indptr, const int32_t *indices, const void *data,
+                           int fp32, int64_t n, int bs, double *inv, int *d_singular,
+                           double *work, hipStream_t s);
+// w -= h v_k with h = reduce(hin); part_out = sum v_next*w (or sum w^2 if v_next == null)
+hipError_t launch_mgs(Red hin, double *hout, double *w, const double *vk, const double *vnext,
+                      int64_t n, double *part_out, int grid, const int *stop_col, int col,
+                      hipStream_t s);
+// h0 = sqrt(reduce(h0)), h1 = sqrt(reduce(w2)); v_next = w * (1/h1) (w if breakdown);
+// workgroup 0 applies the Givens rotations to column col of H and sets the stop flag.
+hipError_t launch_tail(Red h0, Red w2, const double *w, double *vnext, int64_t n, int col,
+                       int m, double *H, double *S, double *giv, GmresState *st, int *stop_map,
+                       int grid, hipStream_t s);
+// v0 = v0 * (1/t), t = sqrt(reduce(p)); S[0] = t, S[1..m] = 0, stop_col = BIG_COL
+hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresState *st,
+                         int grid, hipStream_t s);
+// y = triangular solve (H, S) at stop column; x += y @ V
+hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld,
+                          double *x, int64_t n, int m, const GmresState *st, int grid,
+                          hipStream_t s);
+// dst = sqrt(reduce(p)) if do_sqrt else reduce(p)   (single workgroup)
+hipError_t launch_finalize(Red p, double *dst, int do_sqrt, hipStream_t s);
+// part = sum x^2 (or x*y)
+hipError_t launch_dot(const double *x, const double *y, int64_t n, double *part, int grid,
+                      hipStream_t s);
+hipError_t launch_gather(const double *x, const int32_t *idx, int64_t cnt, double *out,
+                         hipStream_t s);
+// device operator assembly
+hipError_t launch_vlasov_counts(const vtk_vlasov_params &p, int64_t r0, int64_t nrows,
+                                int32_t *counts, hipStream_t s);
+hipError_t launch_vlasov_fill(const vtk_vlasov_params &p, int64_t r0, int64_t nrows,
+                              const int32_t *indptr, int32_t *indices, void *data,
+                              hipStream_t s);
+hipError_t launch_exclusive_scan(const int32_t *in, int32_t *out, int64_t n, void *tmp,
+                                 size_t *tmp_bytes, hipStream_t s);
+hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, int64_t n_local,
+                             const int64_t *halo_cols, int64_t n_halo, hipStream_t s);
+
+int vector_grid(int64_t n);
+
+// ---- host helpers (vtk_host.cpp) -------------------------------------------------------------
+void build_tiles(const std::vector<int32_t> &indptr, int align, std::vector<int32_t> &rows,
+                 bool &has_long, bool &aligned);
+void set_context_free_error(const std::string &msg);
+
+}  // namespace vtk

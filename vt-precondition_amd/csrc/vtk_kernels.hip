@@ -1,0 +1,782 @@
+// vtk_kernels.hip — hand-written gfx950 (MI355X, CDNA4) kernels of the preconditioned-Krylov
+// path.  Built with -ffp-contract=off: every + - * / is one IEEE-rounded operation, so the
+// SpMV row sums (serial, ascending column order — scipy sparsetools csr_matvec), the BJ
+// apply (serial over the block row) and the BJ setup (Gauss-Jordan, partial pivoting) are
+// bit-identical to the CPU restatement in oracle/vtk_oracle.c.
+//
+// Reductions are deterministic: each workgroup of a fixed grid (G <= GMAX, a function of n
+// only) writes one partial; every consumer workgroup sums the G partials in one fixed order,
+// so all workgroups (and all runs) see the same scalar.  No float atomics anywhere.
+//
+// Wavefront = 64 lanes.  Geometry and rooflines: DESIGN.md §3.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <float.h>
+
+#include "vtk_internal.hpp"
+#include "vtk_vlasov.hpp"
+
+namespace vtk {
+
+// ------------------------------------------------------------------------------------------
+// reductions
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;  // lane 0
+}
+
+// every thread of the workgroup returns the same total (fixed order)
+__device__ __forceinline__ double block_sum(double v, double *red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+    return s;
+}
+
+__device__ __forceinline__ double reduce_red(Red r, double *red) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < r.cnt; i += NT) s += r.p[i];
+    return block_sum(s, red);
+}
+
+__device__ __forceinline__ bool stopped(const int *stop_col, int col) {
+    // wave-uniform: one scalar load
+    return stop_col != nullptr && __builtin_nontemporal_load(stop_col) < col;
+}
+
+// ------------------------------------------------------------------------------------------
+// CSR SpMV, CSR-stream tiles: a workgroup stages one tile's products val*x[col] in LDS with
+// fully coalesced reads of data/indices, then one lane per row sums its products serially.
+// Rows longer than TILE_NNZ form single-row tiles reduced by the whole workgroup.
+// ------------------------------------------------------------------------------------------
+template <typename VT, bool HALO>
+struct SpmvK {
+    const int32_t *indptr, *indices;
+    const VT *data;
+    const int32_t *tile_row;
+    int ntiles, n_local;
+    const double *x, *halo;
+    double *y;
+    const double *b, *inv, *v0;
+    double *part0, *part1;
+    const int *stop_col;
+    int col;
+};
+
+template <typename VT, bool HALO>
+__device__ __forceinline__ double xload(const SpmvK<VT, HALO> &a, int c) {
+    if (HALO) return c < a.n_local ? a.x[c] : a.halo[c - a.n_local];
+    return a.x[c];
+}
+
+template <int BS>
+__device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]) {
+    if constexpr (BS % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < BS; j += 2) {
+            const double2 t = *reinterpret_cast<const double2 *>(irow + j);
+            m[j] = t.x;
+            m[j + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < BS; ++j) m[j] = irow[j];
+    }
+}
+
+// EPI: 0 plain, 1 residual, 2 preconditioned (BS == 0: identity, else block-Jacobi of size BS)
+template <typename VT, bool HALO, int EPI, int BS>
+__global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
+    __shared__ double prod[TILE_NNZ];
+    __shared__ int rp[TILE_ROWS + 1];
+    __shared__ double red[NT / 64];
+    if (stopped(a.stop_col, a.col)) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const int r0 = a.tile_row[t], r1 = a.tile_row[t + 1], nr = r1 - r0;
+        const int nz0 = a.indptr[r0], nnz = a.indptr[r1] - nz0;
+        if (nnz <= TILE_NNZ) {
+            for (int i = tid; i <= nr; i += NT) rp[i] = a.indptr[r0 + i] - nz0;
+            const int32_t *ci = a.indices + nz0;
+            const VT *cv = a.data + nz0;
+            int e = tid;
+            for (; e + 3 * NT < nnz; e += 4 * NT) {
+                const int c0 = ci[e], c1 = ci[e + NT], c2 = ci[e + 2 * NT], c3 = ci[e + 3 * NT];
+                const double d0 = (double)cv[e], d1 = (double)cv[e + NT];
+                const double d2 = (double)cv[e + 2 * NT], d3 = (double)cv[e + 3 * NT];
+                const double x0 = xload(a, c0), x1 = xload(a, c1), x2 = xload(a, c2), x3 = xload(a, c3);
+                prod[e] = d0 * x0;
+                prod[e + NT] = d1 * x1;
+                prod[e + 2 * NT] = d2 * x2;
+                prod[e + 3 * NT] = d3 * x3;
+            }
+            for (; e < nnz; e += NT) prod[e] = (double)cv[e] * xload(a, ci[e]);
+            __syncthreads();
+            for (int base = 0; base < nr; base += NT) {
+                const int i = base + tid;
+                const bool act = i < nr;
+                double s = 0.0;
+                if (act) {
+                    const int k1 = rp[i + 1];
+                    for (int k = rp[i]; k < k1; ++k) s += prod[k];
+                }
+                const int row = r0 + i;
+                if constexpr (EPI == EPI_PLAIN) {
+                    if (act) a.y[row] = s;
+                } else if constexpr (EPI == EPI_RESID) {
+                    if (act) {
+                        const double r = a.b[row] - s;
+                        a.y[row] = r;
+                        acc0 += r * r;
+                    }
+                } else {
+                    double z = s;
+                    if constexpr (BS > 0) {
+                        // z_i = sum_j inv[i][j] * y_j over the BS lanes of this block
+                        double m[BS];
+                        if (act) load_inv_row<BS>(a.inv + (size_t)row * BS, m);
+                        const int gb = lane & ~(BS - 1);
+                        z = 0.0;
+#pragma unroll
+                        for (int j = 0; j < BS; ++j) {
+                            const double yj = __shfl(s, gb + j, 64);
+                            if (act) z += m[j] * yj;
+                        }
+                    }
+                    if (act) {
+                        a.y[row] = z;
+                        acc0 += z * z;
+                        if (a.v0) acc1 += a.v0[row] * z;
+                    }
+                }
+            }
+            __syncthreads();
+        } else {
+            // long rows (each such tile is a single row): workgroup-strided products
+            for (int i = 0; i < nr; ++i) {
+                const int row = r0 + i;
+                const int k0 = a.indptr[row], k1 = a.indptr[row + 1];
+                double s = 0.0;
+                for (int k = k0 + tid; k < k1; k += NT) s += (double)a.data[k] * xload(a, a.indices[k]);
+                s = block_sum(s, red);
+                if (tid == 0) {
+                    if constexpr (EPI == EPI_PLAIN) {
+                        a.y[row] = s;
+                    } else if constexpr (EPI == EPI_RESID) {
+                        const double r = a.b[row] - s;
+                        a.y[row] = r;
+                        acc0 += r * r;
+                    } else {
+                        a.y[row] = s;   // BS == 0 only (host guarantees)
+                        acc0 += s * s;
+                        if (a.v0) acc1 += a.v0[row] * s;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (EPI != EPI_PLAIN) {
+        const double t0 = block_sum(acc0, red);
+        if (tid == 0) a.part0[blockIdx.x] = t0;
+        if (EPI == EPI_PREC && a.v0 != nullptr) {
+            const double t1 = block_sum(acc1, red);
+            if (tid == 0) a.part1[blockIdx.x] = t1;
+        }
+    }
+}
+
+template <typename VT, bool HALO>
+static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const double *b,
+                                const double *inv, int bs, const double *v0, double *part0,
+                                double *part1, const int *stop_col, int col, hipStream_t s) {
+    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
+                      in.tiles->d_row, in.tiles->ntiles, in.n_local, in.x, in.halo,
+                      y, b, inv, v0, part0, part1, stop_col, col};
+    const dim3 g(in.tiles->grid), blk(NT);
+    if (epi == EPI_PLAIN) {
+        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1>), g, blk, 0, s, a);
+    } else if (epi == EPI_RESID) {
+        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID, 1>), g, blk, 0, s, a);
+    } else {
+        if (inv == nullptr) bs = 0;
+        switch (bs) {
+            case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 0>), g, blk, 0, s, a); break;
+            case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 1>), g, blk, 0, s, a); break;
+            case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 2>), g, blk, 0, s, a); break;
+            case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 4>), g, blk, 0, s, a); break;
+            case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 8>), g, blk, 0, s, a); break;
+            case 16: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 16>), g, blk, 0, s, a); break;
+            case 32: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 32>), g, blk, 0, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
+                       int bs, const double *v0, double *part0, double *part1,
+                       const int *stop_col, int col, hipStream_t s) {
+    if (in.tiles->ntiles == 0) return hipSuccess;
+    const bool halo = in.halo != nullptr;
+    if (in.fp32) {
+        return halo ? spmv_dispatch<float, true>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s)
+                    : spmv_dispatch<float, false>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s);
+    }
+    return halo ? spmv_dispatch<double, true>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s)
+                : spmv_dispatch<double, false>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// block-Jacobi apply (standalone): one lane per row, serial j order.  inv == null: identity.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_bj_apply(const double *__restrict__ inv, int bs, int64_t n,
+                                                 const double *__restrict__ r, double *__restrict__ z,
+                                                 const double *__restrict__ v0, double *part0,
+                                                 double *part1, const int *stop_col, int col) {
+    __shared__ double red[NT / 64];
+    if (stopped(stop_col, col)) return;
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+        double v;
+        if (inv == nullptr) {
+            v = r[i];
+        } else {
+            const int64_t blk = i / bs;
+            const double *irow = inv + (size_t)i * bs;
+            const int64_t c0 = blk * bs;
+            v = 0.0;
+            for (int j = 0; j < bs; ++j) {
+                const double rv = (c0 + j) < n ? r[c0 + j] : 0.0;
+                v += irow[j] * rv;
+            }
+        }
+        z[i] = v;
+        acc0 += v * v;
+        if (v0) acc1 += v0[i] * v;
+    }
+    if (part0) {
+        const double t0 = block_sum(acc0, red);
+        if (threadIdx.x == 0) part0[blockIdx.x] = t0;
+    }
+    if (part1 && v0) {
+        const double t1 = block_sum(acc1, red);
+        if (threadIdx.x == 0) part1[blockIdx.x] = t1;
+    }
+}
+
+hipError_t launch_bj_apply(const double *inv, int bs, int64_t n, const double *r, double *z,
+                           const double *v0, double *part0, double *part1, int grid,
+                           const int *stop_col, int col, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bj_apply, dim3(grid), dim3(NT), 0, s, inv, bs, n, r, z, v0, part0, part1,
+                       stop_col, col);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// block-Jacobi setup: dense diagonal block, Gauss-Jordan with partial pivoting.
+// BS a power of two <= 64: one lane per block row (BS lanes per block), rows swapped and the
+// pivot row broadcast with cross-lane shuffles, everything in registers.  Same op sequence as
+// orc_bj_setup.  Other bs: one lane per block, block in a global workspace.
+// ------------------------------------------------------------------------------------------
+template <typename VT, int BS>
+__global__ __launch_bounds__(NT) void k_bj_setup(const int32_t *__restrict__ indptr,
+                                                 const int32_t *__restrict__ indices,
+                                                 const VT *__restrict__ data, int64_t n,
+                                                 int64_t nb, double *__restrict__ inv, int *singular) {
+    const int64_t gt = (int64_t)blockIdx.x * NT + threadIdx.x;
+    const int64_t blk = gt / BS;
+    const int ii = (int)(gt % BS);
+    const int lane = threadIdx.x & 63;
+    const int gb = lane & ~(BS - 1);
+    const bool live = blk < nb;
+    const int64_t row = blk * BS + ii;
+    double A[BS], I[BS];
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+        A[j] = 0.0;
+        I[j] = (j == ii) ? 1.0 : 0.0;
+    }
+    if (live) {
+        if (row >= n) {
+#pragma unroll
+            for (int j = 0; j < BS; ++j) if (j == ii) A[j] = 1.0;
+        } else {
+            const int64_t c0 = blk * BS;
+            for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
+                const int64_t c = indices[k] - c0;
+                const double v = (double)data[k];
+#pragma unroll
+                for (int j = 0; j < BS; ++j) if (c == j) A[j] = v;
+            }
+        }
+    }
+    bool sing = false;
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+        // pivot: first row r >= c with the largest |A[r][c]|
+        double best = (ii >= c) ? __builtin_fabs(A[c]) : -1.0;
+        int bidx = ii;
+#pragma unroll
+        for (int off = 1; off < BS; off <<= 1) {
+            const double ob = __shfl_xor(best, off, 64);
+            const int oi = __shfl_xor(bidx, off, 64);
+            if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+        }
+        if (best == 0.0) sing = true;
+        const int piv = bidx;
+        // swap rows c and piv
+#pragma unroll
+        for (int j = 0; j < BS; ++j) {
+            const double ac = __shfl(A[j], gb + c, 64), ap = __shfl(A[j], gb + piv, 64);
+            const double ic = __shfl(I[j], gb + c, 64), ip = __shfl(I[j], gb + piv, 64);
+            if (ii == c) { A[j] = ap; I[j] = ip; }
+            else if (ii == piv) { A[j] = ac; I[j] = ic; }
+        }
+        const double d = __shfl(A[c], gb + c, 64);
+        if (ii == c) {
+#pragma unroll
+            for (int j = 0; j < BS; ++j) { A[j] = A[j] / d; I[j] = I[j] / d; }
+        }
+        const double f = A[c];
+#pragma unroll
+        for (int j = 0; j < BS; ++j) {
+            const double pa = __shfl(A[j], gb + c, 64), pi = __shfl(I[j], gb + c, 64);
+            if (ii != c) { A[j] = A[j] - f * pa; I[j] = I[j] - f * pi; }
+        }
+    }
+    if (live) {
+        if (sing && ii == 0) atomicMin(singular, (int)blk);
+        double *o = inv + (size_t)(blk * BS + ii) * BS;
+#pragma unroll
+        for (int j = 0; j < BS; ++j) o[j] = I[j];
+    }
+}
+
+template <typename VT>
+__global__ __launch_bounds__(NT) void k_bj_setup_generic(const int32_t *__restrict__ indptr,
+                                                         const int32_t *__restrict__ indices,
+                                                         const VT *__restrict__ data, int64_t n,
+                                                         int64_t nb, int bs, double *__restrict__ inv,
+                                                         double *__restrict__ work, int *singular) {
+    const int64_t blk = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (blk >= nb) return;
+    double *A = work + (size_t)blk * bs * bs;
+    double *I = inv + (size_t)blk * bs * bs;
+    for (int k = 0; k < bs * bs; ++k) { A[k] = 0.0; I[k] = 0.0; }
+    for (int i = 0; i < bs; ++i) {
+        const int64_t row = blk * bs + i;
+        I[i * bs + i] = 1.0;
+        if (row >= n) { A[i * bs + i] = 1.0; continue; }
+        for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
+            const int64_t c = indices[k] - blk * bs;
+            if (c >= 0 && c < bs) A[i * bs + c] = (double)data[k];
+        }
+    }
+    for (int c = 0; c < bs; ++c) {
+        int piv = c;
+        double best = __builtin_fabs(A[c * bs + c]);
+        for (int r = c + 1; r < bs; ++r) {
+            const double v = __builtin_fabs(A[r * bs + c]);
+            if (v > best) { best = v; piv = r; }
+        }
+        if (best == 0.0) { atomicMin(singular, (int)blk); return; }
+        if (piv != c) {
+            for (int j = 0; j < bs; ++j) {
+                double t = A[c * bs + j]; A[c * bs + j] = A[piv * bs + j]; A[piv * bs + j] = t;
+                t = I[c * bs + j]; I[c * bs + j] = I[piv * bs + j]; I[piv * bs + j] = t;
+            }
+        }
+        const double d = A[c * bs + c];
+        for (int j = 0; j < bs; ++j) { A[c * bs + j] = A[c * bs + j] / d; I[c * bs + j] = I[c * bs + j] / d; }
+        for (int r = 0; r < bs; ++r) {
+            if (r == c) continue;
+            const double f = A[r * bs + c];
+            for (int j = 0; j < bs; ++j) {
+                A[r * bs + j] = A[r * bs + j] - f * A[c * bs + j];
+                I[r * bs + j] = I[r * bs + j] - f * I[c * bs + j];
+            }
+        }
+    }
+}
+
+template <typename VT>
+static hipError_t bj_setup_t(const int32_t *indptr, const int32_t *indices, const VT *data, int64_t n,
+                             int bs, double *inv, int *sing, double *work, hipStream_t s) {
+    const int64_t nb = (n + bs - 1) / bs;
+    if (nb == 0) return hipSuccess;
+    const int64_t threads = nb * bs;
+    const dim3 g((unsigned)((threads + NT - 1) / NT));
+    switch (bs) {
+        case 1: hipLaunchKernelGGL((k_bj_setup<VT, 1>), g, dim3(NT), 0, s, indptr, indices, data, n, nb, inv, sing); break;
+        case 2: hipLaunchKernelGGL((k_bj_setup<VT, 2>), g, dim3(NT), 0, s, indptr, indices, data, n, nb, inv, sing); break;
+        case 4: hipLaunchKernelGGL((k_bj_setup<VT, 4>), g, dim3(NT), 0, s, indptr, indices, data, n, nb, inv, sing); break;
+        case 8: hipLaunchKernelGGL((k_bj_setup<VT, 8>), g, dim3(NT), 0, s, indptr, indices, data, n, nb, inv, sing); break;
+        case 16: hipLaunchKernelGGL((k_bj_setup<VT, 16>), g, dim3(NT), 0, s, indptr, indices, data, n, nb, inv, sing); break;
+        case 32: hipLaunchKernelGGL((k_bj_setup<VT, 32>), g, dim3(NT), 0, s, indptr, indices, data, n, nb, inv, sing); break;
+        default: {
+            const dim3 gg((unsigned)((nb + NT - 1) / NT));
+            hipLaunchKernelGGL(k_bj_setup_generic<VT>, gg, dim3(NT), 0, s, indptr, indices, data, n, nb,
+                               bs, inv, work, sing);
+        }
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bj_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
+                           int64_t n, int bs, double *inv, int *d_singular, double *work, hipStream_t s) {
+    if (fp32) return bj_setup_t<float>(indptr, indices, static_cast<const float *>(data), n, bs, inv, d_singular, work, s);
+    return bj_setup_t<double>(indptr, indices, static_cast<const double *>(data), n, bs, inv, d_singular, work, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Modified Gram-Schmidt step (iterative.py:756-759): h = <v_k, w> (reduced); w -= h*v_k;
+// fused with the partial <v_{k+1}, w> of the next step (or ||w||^2 after the last one).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_mgs(Red hin, double *hout, double *__restrict__ w,
+                                            const double *__restrict__ vk,
+                                            const double *__restrict__ vn, int64_t n,
+                                            double *part_out, const int *stop_col, int col) {
+    __shared__ double red[NT / 64];
+    if (stopped(stop_col, col)) return;
+    const double h = reduce_red(hin, red);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && hout) *hout = h;
+    double acc = 0.0;
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            double2 wv = *reinterpret_cast<const double2 *>(w + i);
+            const double2 kv = *reinterpret_cast<const double2 *>(vk + i);
+            wv.x = wv.x - h * kv.x;
+            wv.y = wv.y - h * kv.y;
+            *reinterpret_cast<double2 *>(w + i) = wv;
+            if (vn) {
+                const double2 nv = *reinterpret_cast<const double2 *>(vn + i);
+                acc += nv.x * wv.x;
+                acc += nv.y * wv.y;
+            } else {
+                acc += wv.x * wv.x;
+                acc += wv.y * wv.y;
+            }
+        } else {
+            const double wv = w[i] - h * vk[i];
+            w[i] = wv;
+            acc += (vn ? vn[i] : wv) * wv;
+        }
+    }
+    const double t = block_sum(acc, red);
+    if (threadIdx.x == 0) part_out[blockIdx.x] = t;
+}
+
+hipError_t launch_mgs(Red hin, double *hout, double *w, const double *vk, const double *vnext,
+                      int64_t n, double *part_out, int grid, const int *stop_col, int col,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(k_mgs, dim3(grid), dim3(NT), 0, s, hin, hout, w, vk, vnext, n, part_out,
+                       stop_col, col);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// LAPACK 3.10+ dlartg (the lartg SciPy calls, iterative.py:779)
+// ------------------------------------------------------------------------------------------
+__device__ void d_lartg(double f, double g, double &c, double &s, double &r) {
+    const double safmin = DBL_MIN;
+    const double safmax = 1.0 / DBL_MIN;
+    const double rtmin = __builtin_sqrt(safmin);
+    const double rtmax = __builtin_sqrt(safmax / 2.0);
+    const double f1 = __builtin_fabs(f), g1 = __builtin_fabs(g);
+    if (g == 0.0) {
+        c = 1.0; s = 0.0; r = f;
+    } else if (f == 0.0) {
+        c = 0.0; s = __builtin_copysign(1.0, g); r = g1;
+    } else if (f1 > rtmin && f1 < rtmax && g1 > rtmin && g1 < rtmax) {
+        const double d = __builtin_sqrt(f * f + g * g);
+        c = f1 / d;
+        r = __builtin_copysign(d, f);
+        s = g / r;
+    } else {
+        double u = f1 > g1 ? f1 : g1;
+        if (u < safmin) u = safmin;
+        if (u > safmax) u = safmax;
+        const double fs = f / u, gs = g / u;
+        const double d = __builtin_sqrt(fs * fs + gs * gs);
+        c = __builtin_fabs(fs) / d;
+        const double rr = __builtin_copysign(d, f);
+        s = gs / rr;
+        r = rr * u;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Arnoldi tail (iterative.py:761-794): h1 = ||w||, breakdown test, v_{col+1} = w * (1/h1);
+// workgroup 0 / lane 0 rotates column col of H and decides whether the cycle stops.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_tail(Red h0r, Red w2r, const double *__restrict__ w,
+                                             double *__restrict__ vn, int64_t n, int col, int m,
+                                             double *H, double *S, double *giv, GmresState *st,
+                                             int *stop_map) {
+    __shared__ double red[NT / 64];
+    if (st->stop_col < col) return;
+    const double h0 = __builtin_sqrt(reduce_red(h0r, red));
+    const double h1 = __builtin_sqrt(reduce_red(w2r, red));
+    const bool brk = h1 <= DBL_EPSILON * h0;
+    const double sc = brk ? 1.0 : 1.0 / h1;
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            double2 v = *reinterpret_cast<const double2 *>(w + i);
+            v.x = v.x * sc;
+            v.y = v.y * sc;
+            *reinterpret_cast<double2 *>(vn + i) = v;
+        } else {
+            vn[i] = w[i] * sc;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double *hc = H + (size_t)col * (m + 1);
+        hc[col + 1] = brk ? 0.0 : h1;
+        for (int k = 0; k < col; ++k) {
+            const double c = giv[2 * k], s = giv[2 * k + 1];
+            const double n0 = hc[k], n1 = hc[k + 1];
+            hc[k] = c * n0 + s * n1;
+            hc[k + 1] = -s * n0 + c * n1;
+        }
+        double c, s, mag;
+        d_lartg(hc[col], hc[col + 1], c, s, mag);
+        giv[2 * col] = c;
+        giv[2 * col + 1] = s;
+        hc[col] = mag;
+        hc[col + 1] = 0.0;
+        const double t = -s * S[col];
+        S[col] = c * S[col];
+        S[col + 1] = t;
+        const double presid = __builtin_fabs(t);
+        st->presid = presid;
+        st->inner += 1;
+        if (presid <= st->ptol || brk) {
+            st->breakdown = brk ? 1 : 0;
+            st->stop_col = col;
+            if (stop_map) __hip_atomic_store(stop_map, col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+hipError_t launch_tail(Red h0, Red w2, const double *w, double *vnext, int64_t n, int col, int m,
+                       double *H, double *S, double *giv, GmresState *st, int *stop_map, int grid,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_tail, dim3(grid), dim3(NT), 0, s, h0, w2, w, vnext, n, col, m, H, S, giv, st,
+                       stop_map);
+    return hipGetLastError();
+}
+
+// v0 *= 1/t (iterative.py:742-747)
+__global__ __launch_bounds__(NT) void k_scale0(Red p, double *__restrict__ v0, int64_t n, double *S,
+                                               int m, GmresState *st) {
+    __shared__ double red[NT / 64];
+    const double t = __builtin_sqrt(reduce_red(p, red));
+    const double sc = 1.0 / t;
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            double2 v = *reinterpret_cast<const double2 *>(v0 + i);
+            v.x = v.x * sc;
+            v.y = v.y * sc;
+            *reinterpret_cast<double2 *>(v0 + i) = v;
+        } else {
+            v0[i] = v0[i] * sc;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int k = 0; k <= m; ++k) S[k] = 0.0;
+        S[0] = t;
+        st->stop_col = BIG_COL;
+        st->breakdown = 0;
+    }
+}
+
+hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresState *st, int grid,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_scale0, dim3(grid), dim3(NT), 0, s, p, v0, n, S, m, st);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// x += y @ V[0..col] with y from the (m+1) x m Hessenberg least squares
+// (iterative.py:799-814).  Workgroup-redundant triangular solve on lane 0, into LDS.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, const double *__restrict__ S,
+                                                const double *__restrict__ V, int64_t ld,
+                                                double *__restrict__ x, int64_t n, int m,
+                                                const GmresState *st) {
+    extern __shared__ __attribute__((aligned(16))) double ys[];
+    const int col = st->stop_col < m ? st->stop_col : m - 1;
+    if (threadIdx.x == 0) {
+        const int M1 = m + 1;
+        for (int k = 0; k <= col; ++k) ys[k] = S[k];
+        if (H[(size_t)col * M1 + col] == 0.0) ys[col] = 0.0;
+        for (int k = col; k > 0; --k) {
+            if (ys[k] != 0.0) {
+                ys[k] = ys[k] / H[(size_t)k * M1 + k];
+                const double t = ys[k];
+                for (int i = 0; i < k; ++i) ys[i] = ys[i] - t * H[(size_t)k * M1 + i];
+            }
+        }
+        if (ys[0] != 0.0) ys[0] = ys[0] / H[0];
+    }
+    __syncthreads();
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            double ax = 0.0, ay = 0.0;
+            for (int k = 0; k <= col; ++k) {
+                const double2 v = *reinterpret_cast<const double2 *>(V + (size_t)k * ld + i);
+                ax += ys[k] * v.x;
+                ay += ys[k] * v.y;
+            }
+            double2 xv = *reinterpret_cast<const double2 *>(x + i);
+            xv.x = xv.x + ax;
+            xv.y = xv.y + ay;
+            *reinterpret_cast<double2 *>(x + i) = xv;
+        } else {
+            double a = 0.0;
+            for (int k = 0; k <= col; ++k) a += ys[k] * V[(size_t)k * ld + i];
+            x[i] = x[i] + a;
+        }
+    }
+}
+
+hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld, double *x,
+                          int64_t n, int m, const GmresState *st, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_xupdate, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n,
+                       m, st);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(NT) void k_finalize(Red p, double *dst, int do_sqrt) {
+    __shared__ double red[NT / 64];
+    const double t = reduce_red(p, red);
+    if (threadIdx.x == 0) *dst = do_sqrt ? __builtin_sqrt(t) : t;
+}
+
+hipError_t launch_finalize(Red p, double *dst, int do_sqrt, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(NT), 0, s, p, dst, do_sqrt);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(NT) void k_dot(const double *__restrict__ x, const double *__restrict__ y,
+                                            int64_t n, double *part) {
+    __shared__ double red[NT / 64];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+        acc += x[i] * (y ? y[i] : x[i]);
+    const double t = block_sum(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+hipError_t launch_dot(const double *x, const double *y, int64_t n, double *part, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_dot, dim3(grid), dim3(NT), 0, s, x, y, n, part);
+    return hipGetLastError();
+}
+
+__global__ void k_gather(const double *__restrict__ x, const int32_t *__restrict__ idx, int64_t cnt,
+                         double *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = x[idx[i]];
+}
+
+hipError_t launch_gather(const double *x, const int32_t *idx, int64_t cnt, double *out, hipStream_t s) {
+    if (cnt == 0) return hipSuccess;
+    const int g = (int)((cnt + NT - 1) / NT < 1024 ? (cnt + NT - 1) / NT : 1024);
+    hipLaunchKernelGGL(k_gather, dim3(g), dim3(NT), 0, s, x, idx, cnt, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// device-side operator assembly: counts -> exclusive scan -> fill
+// ------------------------------------------------------------------------------------------
+__global__ void k_vlasov_counts(vtk_vlasov_params p, int64_t r0, int64_t nrows, int32_t *counts) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * blockDim.x)
+        counts[i] = vlasov_row_count(p, r0 + i);
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[nrows] = 0;
+}
+
+template <typename VT>
+__global__ void k_vlasov_fill(vtk_vlasov_params p, int64_t r0, int64_t nrows, const int32_t *indptr,
+                              int32_t *indices, VT *data) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * blockDim.x) {
+        VlasovRow row;
+        vlasov_row(p, r0 + i, row);
+        const int32_t o = indptr[i];
+        for (int k = 0; k < row.count; ++k) {
+            indices[o + k] = (int32_t)row.col[k];
+            data[o + k] = (VT)row.val[k];
+        }
+    }
+}
+
+hipError_t launch_vlasov_counts(const vtk_vlasov_params &p, int64_t r0, int64_t nrows, int32_t *counts,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_vlasov_counts, dim3(2048), dim3(NT), 0, s, p, r0, nrows, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_vlasov_fill(const vtk_vlasov_params &p, int64_t r0, int64_t nrows, const int32_t *indptr,
+                              int32_t *indices, void *data, hipStream_t s) {
+    if (p.fp32)
+        hipLaunchKernelGGL(k_vlasov_fill<float>, dim3(2048), dim3(NT), 0, s, p, r0, nrows, indptr, indices,
+                           static_cast<float *>(data));
+    else
+        hipLaunchKernelGGL(k_vlasov_fill<double>, dim3(2048), dim3(NT), 0, s, p, r0, nrows, indptr, indices,
+                           static_cast<double *>(data));
+    return hipGetLastError();
+}
+
+hipError_t launch_exclusive_scan(const int32_t *in, int32_t *out, int64_t n, void *tmp, size_t *tmp_bytes,
+                                 hipStream_t s) {
+    return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
+}
+
+// global column -> local (owned: c - row_begin; halo: n_local + rank in halo_cols)
+__global__ void k_remap(int32_t *indices, int64_t nnz, int64_t row_begin, int64_t n_local,
+                        const int64_t *halo_cols, int64_t n_halo) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = indices[k];
+        const int64_t lc = c - row_begin;
+        if (lc >= 0 && lc < n_local) {
+            indices[k] = (int32_t)lc;
+        } else {
+            int64_t lo = 0, hi = n_halo;   // lower_bound
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (halo_cols[mid] < c) lo = mid + 1; else hi = mid;
+            }
+            indices[k] = (int32_t)(n_local + lo);
+        }
+    }
+}
+
+hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, int64_t n_local,
+                             const int64_t *halo_cols, int64_t n_halo, hipStream_t s) {
+    if (nnz == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_remap, dim3(2048), dim3(NT), 0, s, indices, nnz, row_begin, n_local, halo_cols, n_halo);
+    return hipGetLastError();
+}
+
+int vector_grid(int64_t n) {
+    int64_t g = (n + 2 * NT - 1) / (2 * NT);
+    if (g < 1) g = 1;
+    if (g > GMAX) g = GMAX;
+    return (int)g;
+}
+
+}  // namespace vtk

@@ -1,0 +1,395 @@
+"""vtkrylov — MI355X-native preconditioned Krylov path (CSR SpMV + block-Jacobi + GMRES).
+
+Drop-in for the north_star's "reference scipy.sparse path" (SURVEY.md §8b): the callables
+below keep SciPy's names, argument meaning and error behaviour, and route every operation to
+the gfx950 kernels of ``libvtkrylov.so`` through the C-ABI in ``include/vtkrylov.h``.
+
+    scipy.sparse.csr_matrix((data, indices, indptr), shape)  ->  vtkrylov.csr_matrix(...)
+    A @ x                                                    ->  A @ x   (vtk_spmv)
+    LinearOperator(matvec=block-Jacobi)                      ->  vtkrylov.block_jacobi(A, bs)
+    scipy.sparse.linalg.gmres(A, b, x0, rtol=, atol=,        ->  vtkrylov.gmres(...)
+                              restart=, maxiter=, M=)           (iterative.py:582-841)
+
+Vectors may be NumPy arrays (host; copied in and out) or torch CUDA tensors (device memory,
+used in place).  There is no CPU fallback: without the library or a HIP device every call
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import check, lib
+
+__all__ = ["Context", "default_context", "csr_matrix", "vlasov_operator", "block_jacobi",
+           "gmres", "VlasovParams", "vlasov_params", "rhs_splitmix", "partition_rows",
+           "halo_plan", "device_count", "SolveStats"]
+
+VlasovParams = _abi.VlasovParams
+
+
+def vlasov_params(dim: int, shape, *, fp32=False, vmax=6.0, E0=0.5, nu=0.05, alpha=0.25,
+                  cfl=4.0) -> VlasovParams:
+    s = list(shape) + [0] * (4 - len(shape))
+    return VlasovParams(int(dim), int(bool(fp32)), (C.c_int64 * 4)(*s), vmax, E0, nu, alpha, cfl)
+
+
+def device_count() -> int:
+    n = C.c_int()
+    lib().vtk_device_count(C.byref(n))
+    return n.value
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _is_torch_cuda(x) -> bool:
+    t = type(x)
+    return t.__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+class _Vec:
+    """A vector argument: NumPy (host, kind=HOST) or torch CUDA tensor (device, kind=DEVICE)."""
+
+    def __init__(self, x, n: int, writable=False):
+        if _is_torch_cuda(x):
+            import torch
+            if x.dtype != torch.float64 or not x.is_contiguous() or x.numel() != n:
+                raise ValueError("device vectors must be contiguous float64 tensors of length n")
+            torch.cuda.current_stream(x.device).synchronize()
+            self.kind = _abi.PTR_DEVICE
+            self.ptr = C.c_void_p(x.data_ptr())
+            self.obj = x
+        else:
+            a = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+            if a.shape[0] != n:
+                raise ValueError(f"vector has length {a.shape[0]}, expected {n}")
+            if writable and not a.flags.writeable:
+                a = a.copy()
+            self.kind = _abi.PTR_HOST
+            self.ptr = _np_ptr(a)
+            self.obj = a
+
+
+class Context:
+    """One HIP device + stream (+ optional RCCL communicator).  ``vtk_ctx_create``."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().vtk_ctx_create(int(device), C.byref(h)))
+        self._h = h
+        self.device = device
+        self.rank, self.world = 0, 1
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stream_ptr(self) -> int:
+        s = C.c_void_p()
+        check(lib().vtk_ctx_stream(self._h, C.byref(s)), self._h)
+        return s.value or 0
+
+    def synchronize(self):
+        check(lib().vtk_ctx_synchronize(self._h), self._h)
+
+    def comm_init(self, rank: int, world: int, unique_id: bytes | None):
+        buf = None if unique_id is None else C.create_string_buffer(bytes(unique_id), 128)
+        check(lib().vtk_comm_init(self._h, rank, world, buf), self._h)
+        self.rank, self.world = rank, world
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().vtk_comm_unique_id(buf))
+        return buf.raw
+
+    def set_orth(self, orth: int):
+        check(lib().vtk_gmres_set_orth(self._h, int(orth)), self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vtk_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default = {}
+
+
+def default_context(device: int = 0) -> Context:
+    if device not in _default:
+        _default[device] = Context(device)
+    return _default[device]
+
+
+class CsrOperator:
+    """Device-resident CSR operator (this rank's row block).  ``vtk_csr_create``."""
+
+    def __init__(self, handle, ctx: Context, fp32: bool):
+        self._h = handle
+        self.ctx = ctx
+        self.fp32 = bool(fp32)
+        ng, rb, re_, nnz, nh = (C.c_int64() for _ in range(5))
+        check(lib().vtk_csr_info(handle, C.byref(ng), C.byref(rb), C.byref(re_), C.byref(nnz),
+                                 C.byref(nh)), ctx.handle)
+        self.n_global, self.row_begin, self.row_end = ng.value, rb.value, re_.value
+        self.nnz, self.n_halo = nnz.value, nh.value
+        self.n_local = self.row_end - self.row_begin
+        self.shape = (self.n_global, self.n_global)
+        self.dtype = np.dtype(np.float64)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def matvec(self, x):
+        """y = A x on this rank's rows (sparsetools csr_matvec, bit-identical)."""
+        vx = _Vec(x, self.n_local)
+        if vx.kind == _abi.PTR_DEVICE:
+            import torch
+            y = torch.empty_like(vx.obj)
+            check(lib().vtk_spmv(self._h, vx.ptr, C.c_void_p(y.data_ptr()), vx.kind), self.ctx.handle)
+            self.ctx.synchronize()
+            return y
+        y = np.empty(self.n_local)
+        check(lib().vtk_spmv(self._h, vx.ptr, _np_ptr(y), vx.kind), self.ctx.handle)
+        return y
+
+    def __matmul__(self, x):
+        return self.matvec(x)
+
+    def dot(self, x):
+        return self.matvec(x)
+
+    def download(self):
+        """(indptr, indices[global], data) of this rank's rows, as stored on the device."""
+        ip = np.empty(self.n_local + 1, np.int32)
+        ix = np.empty(max(self.nnz, 1), np.int32)
+        d = np.empty(max(self.nnz, 1), np.float32 if self.fp32 else np.float64)
+        check(lib().vtk_csr_download(self._h, _np_ptr(ip), _np_ptr(ix), _np_ptr(d)), self.ctx.handle)
+        return ip, ix[:self.nnz], d[:self.nnz]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vtk_csr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
+    """Build a device CSR operator from ``(data, indices, indptr)`` or a SciPy sparse matrix.
+
+    With ``offsets`` (world+1 row boundaries) the arrays are this rank's row block with
+    global column indices (multi-GPU); otherwise the whole matrix."""
+    ctx = ctx or default_context()
+    if hasattr(arg, "tocsr"):
+        m = arg.tocsr()
+        if not m.has_sorted_indices:
+            m = m.sorted_indices()
+        data, indices, indptr = m.data, m.indices, m.indptr
+        shape = m.shape
+    else:
+        data, indices, indptr = arg
+    if shape is None or shape[0] != shape[1]:
+        raise ValueError("a square shape is required")
+    data = np.asarray(data)
+    fp32 = data.dtype == np.float32
+    data = np.ascontiguousarray(data, dtype=np.float32 if fp32 else np.float64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    indptr = np.ascontiguousarray(indptr, dtype=np.int32)
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
+    h = C.c_void_p()
+    check(lib().vtk_csr_create(ctx.handle, int(shape[0]), None if offs is None else _np_ptr(offs),
+                               int(indptr[-1]), _np_ptr(indptr), _np_ptr(indices), _np_ptr(data),
+                               int(fp32), _abi.PTR_HOST, C.byref(h)), ctx.handle)
+    return CsrOperator(h, ctx, fp32)
+
+
+def vlasov_operator(params: VlasovParams, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
+    """Generate the Appendix-A Vlasov operator directly in device memory."""
+    ctx = ctx or default_context()
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
+    h = C.c_void_p()
+    check(lib().vtk_csr_create_vlasov(ctx.handle, C.byref(params),
+                                      None if offs is None else _np_ptr(offs), C.byref(h)), ctx.handle)
+    return CsrOperator(h, ctx, bool(params.fp32))
+
+
+class BlockJacobi:
+    """Block-Jacobi preconditioner M = blockdiag(A)^-1 (SciPy: a LinearOperator whose matvec
+    applies the bs x bs diagonal-block inverses).  ``vtk_bjacobi_create``."""
+
+    def __init__(self, A: CsrOperator, bs: int = 8):
+        h = C.c_void_p()
+        check(lib().vtk_bjacobi_create(A.handle, int(bs), C.byref(h)), A.ctx.handle)
+        self._h = h
+        self.A = A
+        self.bs = bs
+        self.shape = A.shape
+        self.dtype = np.dtype(np.float64)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def inverse(self) -> np.ndarray:
+        nb = (self.A.n_local + self.bs - 1) // self.bs
+        inv = np.empty((nb, self.bs, self.bs))
+        check(lib().vtk_bjacobi_inverse(self._h, _np_ptr(inv), _abi.PTR_HOST), self.A.ctx.handle)
+        return inv
+
+    def matvec(self, r):
+        vr = _Vec(r, self.A.n_local)
+        if vr.kind == _abi.PTR_DEVICE:
+            import torch
+            z = torch.empty_like(vr.obj)
+            check(lib().vtk_bjacobi_apply(self._h, vr.ptr, C.c_void_p(z.data_ptr()), vr.kind), self.A.ctx.handle)
+            self.A.ctx.synchronize()
+            return z
+        z = np.empty(self.A.n_local)
+        check(lib().vtk_bjacobi_apply(self._h, vr.ptr, _np_ptr(z), vr.kind), self.A.ctx.handle)
+        return z
+
+    def __matmul__(self, r):
+        return self.matvec(r)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vtk_prec_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def block_jacobi(A: CsrOperator, bs: int = 8) -> BlockJacobi:
+    return BlockJacobi(A, bs)
+
+
+@dataclass
+class SolveStats:
+    inner_iters: int
+    restarts: int
+    presid: float
+    rnorm: float
+    bnorm: float
+    atol_eff: float
+    t_solve: float
+    bytes_moved: float
+    breakdown: int
+    orth: int
+
+
+_last_stats: SolveStats | None = None
+
+
+def last_stats() -> SolveStats | None:
+    return _last_stats
+
+
+def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=None,
+          callback=None, callback_type=None):
+    """``scipy.sparse.linalg.gmres`` on the GPU (iterative.py:582-841, left-preconditioned
+    restarted GMRES with modified Gram-Schmidt).  Returns ``(x, info)``.
+
+    ``A``: a :class:`CsrOperator` or any SciPy sparse matrix (uploaded).  ``M``: None or a
+    :class:`BlockJacobi` built on ``A``; any other preconditioner raises TypeError (no CPU
+    fallback).  ``callback`` is not supported (the Arnoldi loop never returns to the host).
+    """
+    global _last_stats
+    if callback is not None:
+        raise NotImplementedError("vtkrylov.gmres: callbacks would force a host round trip per "
+                                  "Arnoldi step and are not supported")
+    if not isinstance(A, CsrOperator):
+        A = csr_matrix(A)
+    if M is not None and not isinstance(M, BlockJacobi):
+        raise TypeError("vtkrylov.gmres: M must be None or vtkrylov.BlockJacobi")
+    if atol == "legacy" or atol is None or atol < 0:
+        raise ValueError(f"'scipy.sparse.linalg.gmres' called with invalid `atol`={atol}; "
+                         "if set, `atol` must be a real, non-negative number.")
+    n = A.n_local
+    vb = _Vec(b, n)
+    if x0 is None:
+        if vb.kind == _abi.PTR_DEVICE:
+            import torch
+            x = torch.zeros_like(vb.obj)
+        else:
+            x = np.zeros(n)
+    else:
+        if vb.kind == _abi.PTR_DEVICE:
+            x = x0.clone()
+        else:
+            x = np.array(x0, dtype=np.float64, copy=True).reshape(-1)
+    vx = _Vec(x, n, writable=True)
+    x = vx.obj
+    info = C.c_int()
+    st = _abi.Stats()
+    check(lib().vtk_gmres(A.handle, None if M is None else M.handle, vb.ptr, vx.ptr,
+                          float(rtol), float(atol), 0 if restart is None else int(restart),
+                          0 if maxiter is None else int(maxiter), vb.kind, C.byref(info),
+                          C.byref(st)), A.ctx.handle)
+    _last_stats = SolveStats(**st.as_dict())
+    return x, info.value
+
+
+def rhs_splitmix(n: int, seed: int = 0x5EED, r0: int = 0, r1: int | None = None) -> np.ndarray:
+    r1 = n if r1 is None else r1
+    b = np.empty(r1 - r0)
+    check(lib().vtk_rhs_splitmix(seed, r0, r1, _np_ptr(b)))
+    return b
+
+
+def vlasov_generate_host(params: VlasovParams, r0: int = 0, r1: int | None = None):
+    """Host assembly of rows [r0, r1) (the same entry code the device generator runs)."""
+    n, nnz = C.c_int64(), C.c_int64()
+    check(lib().vtk_vlasov_size(C.byref(params), C.byref(n), C.byref(nnz)))
+    r1 = n.value if r1 is None else r1
+    per = {1: 3, 2: 5, 4: 9}[params.dim]
+    cap = max(1, (r1 - r0) * per)
+    ip = np.empty(r1 - r0 + 1, np.int32)
+    ix = np.empty(cap, np.int32)
+    d = np.empty(cap, np.float32 if params.fp32 else np.float64)
+    check(lib().vtk_vlasov_generate(C.byref(params), r0, r1, _np_ptr(ip), _np_ptr(ix), _np_ptr(d)))
+    k = int(ip[-1])
+    return ip, ix[:k].copy(), d[:k].copy()
+
+
+def partition_rows(n: int, world: int, align: int = 1, indptr=None) -> np.ndarray:
+    offs = np.empty(world + 1, np.int64)
+    ip = None if indptr is None else np.ascontiguousarray(indptr, np.int32)
+    check(lib().vtk_partition_rows(n, None if ip is None else _np_ptr(ip), world, align, _np_ptr(offs)))
+    return offs
+
+
+def halo_plan(n_global: int, offsets, rank: int, indices):
+    """(local_indices, halo_cols, halo_count_per_rank) of one rank's row block."""
+    offs = np.ascontiguousarray(offsets, np.int64)
+    world = offs.shape[0] - 1
+    idx = np.ascontiguousarray(indices, np.int32)
+    nh = C.c_int64()
+    check(lib().vtk_halo_plan(n_global, _np_ptr(offs), world, rank, idx.shape[0], _np_ptr(idx),
+                              None, C.byref(nh), None, None))
+    loc = np.empty(idx.shape[0], np.int32)
+    cols = np.empty(max(nh.value, 1), np.int64)
+    cnt = np.empty(world, np.int64)
+    check(lib().vtk_halo_plan(n_global, _np_ptr(offs), world, rank, idx.shape[0], _np_ptr(idx),
+                              _np_ptr(loc), C.byref(nh), _np_ptr(cols), _np_ptr(cnt)))
+    return loc, cols[:nh.value], cnt

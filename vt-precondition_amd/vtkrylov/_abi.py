@@ -1,0 +1,126 @@
+"""Raw ctypes binding of libvtkrylov.so (include/vtkrylov.h).
+
+This is the reference-side binding INTEGRATION.md describes: the thin layer a caller of the
+scipy.sparse path adds to reach the gfx950 kernels.  It loads the in-tree library
+(``vtkrylov/lib/libvtkrylov.so``) and nothing else; there is no CPU fallback — if the
+library is missing or no HIP device is visible, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libvtkrylov.so")
+
+OK = 0
+ERR_ARG = -1
+ERR_HIP = -2
+ERR_RCCL = -3
+ERR_SINGULAR = -4
+ERR_NOMEM = -5
+ERR_STATE = -6
+ERR_NODEVICE = -7
+
+PTR_HOST = 0
+PTR_DEVICE = 1
+
+ORTH_MGS = 0
+ORTH_CGS2 = 1
+
+
+class VlasovParams(C.Structure):
+    _fields_ = [("dim", C.c_int), ("fp32", C.c_int), ("shape", C.c_int64 * 4),
+                ("vmax", C.c_double), ("E0", C.c_double), ("nu", C.c_double),
+                ("alpha", C.c_double), ("cfl", C.c_double)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("inner_iters", C.c_int64), ("restarts", C.c_int64), ("presid", C.c_double),
+                ("rnorm", C.c_double), ("bnorm", C.c_double), ("atol_eff", C.c_double),
+                ("t_solve", C.c_double), ("bytes_moved", C.c_double), ("breakdown", C.c_int),
+                ("orth", C.c_int)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+P = C.c_void_p
+I32P = C.POINTER(C.c_int32)
+I64P = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); must cover every function declared in include/vtkrylov.h
+PROTOTYPES = {
+    "vtk_abi_version": (C.c_int, []),
+    "vtk_status_string": (C.c_char_p, [C.c_int]),
+    "vtk_last_error": (C.c_int, [P, C.c_char_p, C.c_size_t]),
+    "vtk_vlasov_size": (C.c_int, [C.POINTER(VlasovParams), I64P, I64P]),
+    "vtk_vlasov_generate": (C.c_int, [C.POINTER(VlasovParams), C.c_int64, C.c_int64, P, P, P]),
+    "vtk_rhs_splitmix": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, P]),
+    "vtk_partition_rows": (C.c_int, [C.c_int64, P, C.c_int, C.c_int, P]),
+    "vtk_halo_plan": (C.c_int, [C.c_int64, P, C.c_int, C.c_int, C.c_int64, P, P, I64P, P, P]),
+    "vtk_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "vtk_ctx_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "vtk_ctx_destroy": (None, [P]),
+    "vtk_ctx_stream": (C.c_int, [P, C.POINTER(P)]),
+    "vtk_ctx_synchronize": (C.c_int, [P]),
+    "vtk_comm_unique_id": (C.c_int, [P]),
+    "vtk_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
+    "vtk_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "vtk_csr_create": (C.c_int, [P, C.c_int64, P, C.c_int64, P, P, P, C.c_int, C.c_int, C.POINTER(P)]),
+    "vtk_csr_create_vlasov": (C.c_int, [P, C.POINTER(VlasovParams), P, C.POINTER(P)]),
+    "vtk_csr_info": (C.c_int, [P, I64P, I64P, I64P, I64P, I64P]),
+    "vtk_csr_download": (C.c_int, [P, P, P, P]),
+    "vtk_csr_destroy": (None, [P]),
+    "vtk_spmv": (C.c_int, [P, P, P, C.c_int]),
+    "vtk_bjacobi_create": (C.c_int, [P, C.c_int, C.POINTER(P)]),
+    "vtk_bjacobi_inverse": (C.c_int, [P, P, C.c_int]),
+    "vtk_bjacobi_apply": (C.c_int, [P, P, P, C.c_int]),
+    "vtk_prec_destroy": (None, [P]),
+    "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
+                            C.POINTER(C.c_int), C.POINTER(Stats)]),
+    "vtk_gmres_set_orth": (C.c_int, [P, C.c_int]),
+}
+
+_lib = None
+
+
+class VtkError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"{msg} (status {status})")
+        self.status = status
+
+
+def lib() -> C.CDLL:
+    """Load libvtkrylov.so (build it with ``make -C vt-precondition_amd/csrc``)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libvtkrylov.so not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.vtk_abi_version() != 1:
+            raise ImportError("libvtkrylov.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error(ctx=None) -> str:
+    buf = C.create_string_buffer(1024)
+    lib().vtk_last_error(ctx, buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(status: int, ctx=None):
+    if status == OK:
+        return
+    import numpy as np
+    msg = last_error(ctx)
+    if status == ERR_SINGULAR:
+        raise np.linalg.LinAlgError(msg)
+    if status == ERR_ARG:
+        raise ValueError(msg)
+    raise VtkError(status, msg or lib().vtk_status_string(status).decode())
