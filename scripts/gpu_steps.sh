@@ -1,0 +1,30 @@
+#!/bin/bash
+# Run GPU steps on the gpurun box, each under its own time limit; stop at the first crash,
+# abort, fault or timeout (test failures, exit 1, do not stop the chain).
+#   scripts/gpu_steps.sh smoke tests bench prof ...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+    local name=$1 to=$2; shift 2
+    echo "== $name: $*"
+    local t0=$(date +%s)
+    timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc ($(( $(date +%s) - t0 ))s)"
+    tail -n 15 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!! fatal rc=$rc: stopping"; exit $rc; fi
+    return 0
+}
+for s in "$@"; do
+    case $s in
+        smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+        testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        bench) step bench 600 python bench.py ;;
+        benchq) step benchq 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done

@@ -95,6 +95,13 @@ def lib() -> C.CDLL:
     """Load libvtkrylov.so (build it with ``make -C vt-precondition_amd/csrc``)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch's libtorch_hip NEEDs "libamdhip64.so" while this
+        # library NEEDs the SONAME "libamdhip64.so.7"; if torch is present it must be loaded
+        # first so both resolve to the same runtime (otherwise torch finds no GPU).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libvtkrylov.so not built: {LIB_PATH} (run __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
