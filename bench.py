@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--spmv-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-inner", type=int, default=20)
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     args = ap.parse_args()
 
     import numpy as np
@@ -112,14 +114,17 @@ def main():
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
 
     import vtkrylov as vk
-    ctx = vk.Context(local)
+    from vtkrylov import comm as vkcomm
+    ndev = vk.device_count()
+    device = local % max(ndev, 1)
+    ctx = vk.Context(device)
     if world > 1:
-        uid = vk.Context.unique_id() if rank == 0 else bytes(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, 0)
-        ctx.comm_init(rank, world, bytes(t.tolist()))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.comm == "rccl":
+            vkcomm.init_rccl(ctx, rank, world)
+        else:
+            vkcomm.init_host(ctx, rank, world)
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
 
     dim, shape, fp32 = CONFIGS[args.config]
     params = vk.vlasov_params(dim, shape, fp32=fp32)
@@ -204,7 +209,7 @@ def main():
         "config": {"workload": f"{args.config}: GMRES({args.restart})+BJ({args.bs}) to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "bs": args.bs, "rtol": args.rtol, "parallelism": f"row-slab x{world}"},
+                   "bs": args.bs, "rtol": args.rtol, "parallelism": f"row-slab x{world}", "comm": args.comm if world > 1 else None},
         "inner_iters_per_solve": iters / args.steps,
         "info": infos,
         "true_rel_residual": rel_res,

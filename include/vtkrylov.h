@@ -115,6 +115,19 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
 /* rank 0 creates the 128-byte RCCL unique id; the caller broadcasts it (any transport) */
 int vtk_comm_unique_id(void *out128);
 int vtk_comm_init(vtk_ctx *ctx, int rank, int world, const void *rccl_unique_id);
+/* Host-staged communicator (test/debug transport, e.g. several ranks sharing one GPU, which
+ * RCCL refuses): the library synchronises its stream, copies the payload to host memory, calls
+ * these hooks and copies the result back.  Counts and offsets are in elements.  Each hook
+ * returns 0 on success.  The production path is RCCL (vtk_comm_init). */
+typedef struct {
+    void *user;
+    int (*allreduce_sum_f64)(void *user, double *buf, int64_t count);
+    int (*alltoallv)(void *user, const void *sendbuf, const int64_t *send_counts,
+                     const int64_t *send_offsets, void *recvbuf, const int64_t *recv_counts,
+                     const int64_t *recv_offsets, int64_t elem_bytes);
+    int (*allgather)(void *user, const void *sendbuf, void *recvbuf, int64_t bytes_per_rank);
+} vtk_host_comm;
+int vtk_comm_init_host(vtk_ctx *ctx, int rank, int world, const vtk_host_comm *ops);
 int vtk_comm_info(vtk_ctx *ctx, int *rank, int *world);
 
 /* ---- operator ------------------------------------------------------------------------ */

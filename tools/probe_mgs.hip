@@ -35,11 +35,12 @@ __global__ __launch_bounds__(NT) void k_mgs(const double *hp, int G, double *__r
         if (MODE == 2 || MODE == 3) wv = __builtin_nontemporal_load((const d2 *)(w + i));
         else wv = *(const d2 *)(w + i);
         if (MODE == 1 || MODE == 2) { kv = __builtin_nontemporal_load((const d2 *)(vk + i)); nv = __builtin_nontemporal_load((const d2 *)(vn + i)); }
-        else if (MODE == 4) { kv = __builtin_nontemporal_load((const d2 *)(vk + i)); nv = *(const d2 *)(vn + i); }
+        else if (MODE >= 4) { kv = __builtin_nontemporal_load((const d2 *)(vk + i)); nv = *(const d2 *)(vn + i); }
         else { kv = *(const d2 *)(vk + i); nv = *(const d2 *)(vn + i); }
         wv.x = wv.x - h * kv.x;
         wv.y = wv.y - h * kv.y;
-        if (MODE == 2) __builtin_nontemporal_store(wv, (d2 *)(w + i));
+        if (MODE == 2 || MODE == 6) __builtin_nontemporal_store(wv, (d2 *)(w + i));
+        else if (MODE == 5) { /* read-only: no store */ }
         else *(d2 *)(w + i) = wv;
         acc += nv.x * wv.x;
         acc += nv.y * wv.y;
@@ -91,8 +92,8 @@ int main(int argc, char **argv) {
     const double bytes_mid = 32.0 * n;
     for (int G : {1024}) {
         for (int rep = 0; rep < 2; ++rep) {
-            for (int alt = 0; alt < 2; ++alt) {
-            for (int mode : {0, 1, 4}) {
+            for (int alt = 0; alt < 1; ++alt) {
+            for (int mode : {4, 5, 6}) {
                 CK(hipMemsetAsync(junk, rep, 1L << 30, s));   // flush caches
                 std::vector<float> per;
                 float t = 0;
@@ -100,6 +101,8 @@ int main(int argc, char **argv) {
                     case 0: t = run_chain<0>(w, V, ld, n, J, G, part, s, per, alt); break;
                     case 1: t = run_chain<1>(w, V, ld, n, J, G, part, s, per, alt); break;
                     case 4: t = run_chain<4>(w, V, ld, n, J, G, part, s, per, alt); break;
+                    case 5: t = run_chain<5>(w, V, ld, n, J, G, part, s, per, alt); break;
+                    case 6: t = run_chain<6>(w, V, ld, n, J, G, part, s, per, alt); break;
                 }
                 std::vector<float> q(per.begin() + 1, per.end());
                 std::sort(q.begin(), q.end());

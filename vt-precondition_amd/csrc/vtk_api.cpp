@@ -84,7 +84,64 @@ int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tile
     return VTK_OK;
 }
 
-// partial sums -> consumer view; across ranks: finalise to a scalar slot + RCCL all-reduce
+// ---- communicator primitives: RCCL on the context stream, or host-staged hooks ------------
+
+// in-place sum over ranks of `count` doubles in device memory
+int comm_allreduce(vtk_ctx *c, double *d, int64_t count) {
+    if (c->host_comm) {
+        std::vector<double> h((size_t)count);
+        HIPCHK(c, hipMemcpyAsync(h.data(), d, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->hops.allreduce_sum_f64(c->hops.user, h.data(), count) != 0) return fail(c, VTK_ERR_STATE, "host allreduce hook failed");
+        HIPCHK(c, hipMemcpyAsync(d, h.data(), count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return VTK_OK;
+    }
+    NCCLCHK(c, ncclAllReduce(d, d, (size_t)count, ncclDouble, ncclSum, c->comm, c->stream));
+    return VTK_OK;
+}
+
+// point-to-point exchange: to rank q scnt[q] elements from send+soff[q], from rank q rcnt[q]
+// elements into recv+roff[q] (ncclSend/ncclRecv in one group: xGMI is point-to-point)
+int comm_alltoallv(vtk_ctx *c, const void *send, const std::vector<int64_t> &scnt, const std::vector<int64_t> &soff,
+                   void *recv, const std::vector<int64_t> &rcnt, const std::vector<int64_t> &roff, ncclDataType_t dt, size_t eb) {
+    const int W = c->world;
+    if (c->host_comm) {
+        const int64_t ns = W ? soff[W - 1] + scnt[W - 1] : 0, nr = W ? roff[W - 1] + rcnt[W - 1] : 0;
+        std::vector<char> hs((size_t)std::max<int64_t>(ns, 1) * eb), hr((size_t)std::max<int64_t>(nr, 1) * eb);
+        if (ns) HIPCHK(c, hipMemcpyAsync(hs.data(), send, ns * eb, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->hops.alltoallv(c->hops.user, hs.data(), scnt.data(), soff.data(), hr.data(), rcnt.data(), roff.data(), (int64_t)eb) != 0)
+            return fail(c, VTK_ERR_STATE, "host alltoallv hook failed");
+        if (nr) HIPCHK(c, hipMemcpyAsync(recv, hr.data(), nr * eb, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return VTK_OK;
+    }
+    NCCLCHK(c, ncclGroupStart());
+    for (int q = 0; q < W; ++q) {
+        if (scnt[q] > 0) NCCLCHK(c, ncclSend((const char *)send + soff[q] * eb, (size_t)scnt[q], dt, q, c->comm, c->stream));
+        if (rcnt[q] > 0) NCCLCHK(c, ncclRecv((char *)recv + roff[q] * eb, (size_t)rcnt[q], dt, q, c->comm, c->stream));
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    return VTK_OK;
+}
+
+// every rank contributes `count` int64 (device), receives world*count (device)
+int comm_allgather_i64(vtk_ctx *c, const int64_t *send, int64_t *recv, int64_t count) {
+    if (c->host_comm) {
+        std::vector<int64_t> hs((size_t)count), hr((size_t)count * c->world);
+        HIPCHK(c, hipMemcpyAsync(hs.data(), send, count * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->hops.allgather(c->hops.user, hs.data(), hr.data(), count * 8) != 0) return fail(c, VTK_ERR_STATE, "host allgather hook failed");
+        HIPCHK(c, hipMemcpyAsync(recv, hr.data(), hr.size() * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return VTK_OK;
+    }
+    NCCLCHK(c, ncclAllGather(send, recv, (size_t)count, ncclInt64, c->comm, c->stream));
+    return VTK_OK;
+}
+
+// partial sums -> consumer view; across ranks: finalise to a scalar slot + all-reduce
 Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
     rc = VTK_OK;
     if (c->world == 1) return Red{part, cnt};
@@ -92,8 +149,7 @@ Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
     double *dst = c->d_scal + (slot++ & 255);
     hipError_t e = launch_finalize(Red{part, cnt}, dst, 0, c->stream);
     if (e != hipSuccess) { rc = fail(c, VTK_ERR_HIP, hipGetErrorString(e)); return Red{dst, 1}; }
-    ncclResult_t r = ncclAllReduce(dst, dst, 1, ncclDouble, ncclSum, c->comm, c->stream);
-    if (r != ncclSuccess) rc = fail(c, VTK_ERR_RCCL, ncclGetErrorString(r));
+    rc = comm_allreduce(c, dst, 1);
     return Red{dst, 1};
 }
 
@@ -101,15 +157,7 @@ int halo_exchange(vtk_csr *A, const double *x) {
     vtk_ctx *c = A->ctx;
     if (c->world == 1) return VTK_OK;
     HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
-    NCCLCHK(c, ncclGroupStart());
-    for (int q = 0; q < c->world; ++q) {
-        if (A->send_cnt[q] > 0)
-            NCCLCHK(c, ncclSend(A->d_send_buf + A->send_off[q], (size_t)A->send_cnt[q], ncclDouble, q, c->comm, c->stream));
-        if (A->recv_cnt[q] > 0)
-            NCCLCHK(c, ncclRecv(A->d_halo + A->recv_off[q], (size_t)A->recv_cnt[q], ncclDouble, q, c->comm, c->stream));
-    }
-    NCCLCHK(c, ncclGroupEnd());
-    return VTK_OK;
+    return comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble, sizeof(double));
 }
 
 SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x) {
@@ -146,7 +194,7 @@ int setup_halo(vtk_csr *A) {
     TRY(dalloc(c, dcnt, W * sizeof(int64_t)));
     TRY(dalloc(c, dall, (size_t)W * W * sizeof(int64_t)));
     HIPCHK(c, hipMemcpyAsync(dcnt.p, A->recv_cnt.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-    NCCLCHK(c, ncclAllGather(dcnt.p, dall.p, W, ncclInt64, c->comm, c->stream));
+    TRY(comm_allgather_i64(c, dcnt.as<int64_t>(), dall.as<int64_t>(), W));
     std::vector<int64_t> all((size_t)W * W);
     HIPCHK(c, hipMemcpyAsync(all.data(), dall.p, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -160,14 +208,8 @@ int setup_halo(vtk_csr *A) {
     TRY(dalloc(c, dreq, (size_t)nh * sizeof(int64_t)));
     TRY(dalloc(c, dsend, (size_t)A->n_send * sizeof(int64_t)));
     if (nh) HIPCHK(c, hipMemcpyAsync(dreq.p, A->halo_cols.data(), nh * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-    NCCLCHK(c, ncclGroupStart());
-    for (int q = 0; q < W; ++q) {
-        if (A->recv_cnt[q] > 0)
-            NCCLCHK(c, ncclSend(dreq.as<int64_t>() + A->recv_off[q], (size_t)A->recv_cnt[q], ncclInt64, q, c->comm, c->stream));
-        if (A->send_cnt[q] > 0)
-            NCCLCHK(c, ncclRecv(dsend.as<int64_t>() + A->send_off[q], (size_t)A->send_cnt[q], ncclInt64, q, c->comm, c->stream));
-    }
-    NCCLCHK(c, ncclGroupEnd());
+    // requests travel opposite to the data: send my recv list to each owner
+    TRY(comm_alltoallv(c, dreq.p, A->recv_cnt, A->recv_off, dsend.p, A->send_cnt, A->send_off, ncclInt64, sizeof(int64_t)));
     std::vector<int64_t> sg((size_t)A->n_send);
     if (A->n_send) HIPCHK(c, hipMemcpyAsync(sg.data(), dsend.p, A->n_send * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -371,7 +413,11 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             enq = col + 1;
             if (col >= LOOKAHEAD) {
                 HIPCHK(c, hipEventSynchronize(ev[(col - LOOKAHEAD) % (LOOKAHEAD + 1)]));
-                if (*mirror < BIG_COL) break;   // stopped: no further columns needed
+                // Act only on a stop at a column whose tail every rank has completed (it is
+                // behind the event just synchronised): a later column's flag may already be
+                // visible on one rank and not on another, and the ranks must enqueue the same
+                // sequence of collectives.
+                if (*mirror <= col - LOOKAHEAD) break;
             }
         }
         (void)enq;
@@ -499,6 +545,18 @@ int vtk_comm_init(vtk_ctx *c, int rank, int world, const void *uid) {
     NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
     c->rank = rank;
     c->world = world;
+    return VTK_OK;
+}
+
+int vtk_comm_init_host(vtk_ctx *c, int rank, int world, const vtk_host_comm *ops) {
+    if (!c || world < 1 || rank < 0 || rank >= world) return fail(c, VTK_ERR_ARG, "vtk_comm_init_host: bad rank/world");
+    if (world > 1 && (!ops || !ops->allreduce_sum_f64 || !ops->alltoallv || !ops->allgather))
+        return fail(c, VTK_ERR_ARG, "vtk_comm_init_host: all three hooks are required");
+    if (c->comm) return fail(c, VTK_ERR_STATE, "vtk_comm_init_host: RCCL communicator already set");
+    c->rank = rank;
+    c->world = world;
+    c->host_comm = world > 1;
+    if (ops) c->hops = *ops;
     return VTK_OK;
 }
 

@@ -55,7 +55,9 @@ struct vtk_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int rank = 0, world = 1;
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;            // RCCL (production transport)
+    bool host_comm = false;               // host-staged hooks (vtk_comm_init_host)
+    vtk_host_comm hops{};
     int orth = VTK_ORTH_MGS;
     // scratch shared by calls on this context
     double *d_part = nullptr;        // [8][GMAX] partial sums

@@ -52,10 +52,10 @@ __device__ __forceinline__ bool stopped(const int *stop_col, int col) {
     return stop_col != nullptr && __builtin_nontemporal_load(stop_col) < col;
 }
 
-// Streamed-once operands (CSR values/indices, BJ inverses, the basis vector being subtracted)
-// are loaded non-temporal so that the vectors reused across consecutive kernels (w, the
-// gathered x) stay resident in the 256 MB Infinity Cache: on C3 (20M rows) this took an MGS
-// step from 122 us to 98 us (tools/probe_mgs.hip).
+// The basis vector an MGS step subtracts (and the basis read by the x update) is loaded
+// non-temporal, 16 B per lane, so that w stays resident in the 256 MB Infinity Cache across
+// the chain of MGS kernels: on C3 (20M rows) an MGS step went from 122 us to 98 us
+// (tools/probe_mgs.hip).  Narrow (4/8 B) nt loads are slow on gfx950; the SpMV keeps plain loads.
 typedef double d2v __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ __forceinline__ T ldnt(const T *p) { return __builtin_nontemporal_load(p); }
@@ -93,13 +93,13 @@ __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]
     if constexpr (BS % 2 == 0) {
 #pragma unroll
         for (int j = 0; j < BS; j += 2) {
-            const d2v t = ldnt2(irow + j);
+            const double2 t = *reinterpret_cast<const double2 *>(irow + j);
             m[j] = t.x;
             m[j + 1] = t.y;
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < BS; ++j) m[j] = ldnt(irow + j);
+        for (int j = 0; j < BS; ++j) m[j] = irow[j];
     }
 }
 
@@ -117,23 +117,26 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
         const int r0 = a.tile_row[t], r1 = a.tile_row[t + 1], nr = r1 - r0;
         const int nz0 = a.indptr[r0], nnz = a.indptr[r1] - nz0;
         if (nnz <= TILE_NNZ) {
-            for (int i = tid; i <= nr; i += NT) rp[i] = ldnt(a.indptr + r0 + i) - nz0;
+            // Plain (cached) loads here: non-temporal 4/8-byte loads ran this kernel 25% slower
+            // (tools/probe_fused.hip: 603 -> 751 us on C3), and neither prefetching the BJ rows
+            // nor a deeper unroll helped.
+            for (int i = tid; i <= nr; i += NT) rp[i] = a.indptr[r0 + i] - nz0;
             const int32_t *ci = a.indices + nz0;
             const VT *cv = a.data + nz0;
             int e = tid;
-            constexpr int U = 8;   // 8 index + 8 value loads in flight per lane
+            constexpr int U = 4;
             for (; e + (U - 1) * NT < nnz; e += U * NT) {
                 int c[U];
                 double d[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    c[u] = ldnt(ci + e + u * NT);
-                    d[u] = (double)ldnt(cv + e + u * NT);
+                    c[u] = ci[e + u * NT];
+                    d[u] = (double)cv[e + u * NT];
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) prod[e + u * NT] = d[u] * xload(a, c[u]);
             }
-            for (; e < nnz; e += NT) prod[e] = (double)ldnt(cv + e) * xload(a, ldnt(ci + e));
+            for (; e < nnz; e += NT) prod[e] = (double)cv[e] * xload(a, ci[e]);
             __syncthreads();
             for (int base = 0; base < nr; base += NT) {
                 const int i = base + tid;
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
                     if (act) {
                         a.y[row] = z;
                         acc0 += z * z;
-                        if (a.v0) acc1 += ldnt(a.v0 + row) * z;
+                        if (a.v0) acc1 += a.v0[row] * z;
                     }
                 }
             }

@@ -108,6 +108,11 @@ class Context:
         check(lib().vtk_comm_unique_id(buf))
         return buf.raw
 
+    def comm_init_host(self, rank: int, world: int, group=None):
+        """Host-staged communicator over torch.distributed (tests; ranks may share a GPU)."""
+        from .comm import init_host
+        return init_host(self, rank, world, group)
+
     def set_orth(self, orth: int):
         check(lib().vtk_gmres_set_orth(self._h, int(orth)), self._h)
 
@@ -318,10 +323,10 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     if callback is not None:
         raise NotImplementedError("vtkrylov.gmres: callbacks would force a host round trip per "
                                   "Arnoldi step and are not supported")
-    if not isinstance(A, CsrOperator):
-        A = csr_matrix(A)
     if M is not None and not isinstance(M, BlockJacobi):
         raise TypeError("vtkrylov.gmres: M must be None or vtkrylov.BlockJacobi")
+    if not isinstance(A, CsrOperator):
+        A = csr_matrix(A)
     if atol == "legacy" or atol is None or atol < 0:
         raise ValueError(f"'scipy.sparse.linalg.gmres' called with invalid `atol`={atol}; "
                          "if set, `atol` must be a real, non-negative number.")

@@ -67,6 +67,8 @@ PROTOTYPES = {
     "vtk_comm_unique_id": (C.c_int, [P]),
     "vtk_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
     "vtk_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    # vtk_comm_init_host: prototype registered by vtkrylov/comm.py (needs the hook struct)
+    "vtk_comm_init_host": (C.c_int, [P, C.c_int, C.c_int, P]),
     "vtk_csr_create": (C.c_int, [P, C.c_int64, P, C.c_int64, P, P, P, C.c_int, C.c_int, C.POINTER(P)]),
     "vtk_csr_create_vlasov": (C.c_int, [P, C.POINTER(VlasovParams), P, C.POINTER(P)]),
     "vtk_csr_info": (C.c_int, [P, I64P, I64P, I64P, I64P, I64P]),
