@@ -192,34 +192,18 @@ def main():
     B = spmv_bytes(A.nnz, A.n_local, fp32)
     spmv_gbs = B / t_spmv / 1e9
 
+    # ---- per-kernel profile of one more solve (outside the timed region): HIP events around
+    #      every launch on the context's stream, algorithmic bytes per launch
+    ctx.profile(True)
+    solve()
+    kprof = ctx.profile_read()
+    ctx.profile(False)
+    tot_s = sum(v["seconds"] for v in kprof.values()) or 1.0
+    dom = max(kprof, key=lambda k: kprof[k]["seconds"])
+    traffic = pmc_traffic(dom, args.config, world)
+    dk = kprof[dom]
+
     ms = elapsed / args.steps * 1e3
-    out = {
-        "metric": "precond-GMRES iters/sec + CSR SpMV achieved-HBM-GB/s, 1/2/4/8 MI355X",
-        "value": iters / elapsed,
-        "unit": "iters/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f64" if not fp32 else "f32-values/f64",
-        "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
-        "config": {"workload": f"{args.config}: GMRES({args.restart})+BJ({args.bs}) to rtol={args.rtol}, "
-                               f"n={n_glob}, row-sharded over {world} GPU(s)",
-                   "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "bs": args.bs, "rtol": args.rtol, "parallelism": f"row-slab x{world}", "comm": args.comm if world > 1 else None},
-        "inner_iters_per_solve": iters / args.steps,
-        "info": infos,
-        "true_rel_residual": rel_res,
-        "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6,
-                 "bytes": B},
-        "roofline": {"kernel": "k_spmv (CSR-stream, plain)", "bound": "hbm", "achieved": spmv_gbs,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": spmv_gbs / HBM_PEAK_GBS,
-                     "traffic": None},
-        "cpu_baseline": None,
-    }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             A_host = A.download()
@@ -231,6 +215,21 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(cls, config, world):
+    """HBM bytes per launch of kernel class `cls` from the newest committed rocprofv3 PMC
+    summary (profiles/rNN_pmc_traffic.json, tools/pmc_summary.py) of this same command
+    (C3, one GPU); None when no summary matches."""
+    import glob
+    if config != "C3" or world != 1:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        k = json.load(f)["kernels"].get(cls)
+    return None if k is None else k["hbm_bytes_per_launch"]
 
 
 def params_nnz(dim, shape):

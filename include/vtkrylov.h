@@ -165,6 +165,21 @@ int vtk_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
               int restart, int64_t maxiter, int ptr_kind, int *info, vtk_stats *stats);
 int vtk_gmres_set_orth(vtk_ctx *ctx, int orth);
 
+/* ---- kernel profile (measurement) ------------------------------------------
+ * When enabled, every kernel the library launches is bracketed by HIP events on the
+ * context's stream; per kernel class the driver accumulates launches, device seconds and the
+ * ALGORITHMIC bytes of each launch (the per-unit figures of SURVEY.md §8d).  No-op launches
+ * after a cycle's stop column are not counted.  Costs ~a few us per launch: not for timing
+ * whole solves. */
+typedef struct {
+    char name[32];       /* kernel class, e.g. "spmv_bj", "mgs", "tail", "spmv"        */
+    int64_t launches;
+    double seconds;      /* sum of event-measured durations                            */
+    double bytes;        /* sum of algorithmic bytes                                   */
+} vtk_kernel_profile;
+int vtk_profile_enable(vtk_ctx *ctx, int on);   /* on: also clears the counters */
+int vtk_profile_read(vtk_ctx *ctx, vtk_kernel_profile *out, int max_entries, int *n_entries);
+
 #ifdef __cplusplus
 }
 #endif

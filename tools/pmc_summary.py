@@ -1,0 +1,80 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/ (committed, cited by bench.py / DESIGN.md).
+
+    python tools/pmc_summary.py --round r01 [--src gpurun_out]
+
+Reads  <src>/prof/run_kernel_stats.csv            (rocprofv3 --kernel-trace --stats)
+       <src>/pmc_fetch/run_counter_collection.csv  (rocprofv3 --pmc FETCH_SIZE)
+       <src>/pmc_write/run_counter_collection.csv  (rocprofv3 --pmc WRITE_SIZE)
+Writes profiles/<round>_kernel_stats.csv (copy) and profiles/<round>_pmc_traffic.json:
+per kernel the mean FETCH_SIZE / WRITE_SIZE per dispatch (KiB) and the corrected HBM bytes
+per launch, following MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of the bytes of a wide
+coalesced streaming read on gfx950 -> x2; WRITE_SIZE is exact for 16-B/lane stores.  Values
+are per dispatch of the same command, so they compare directly with bench.py's per-launch
+algorithmic bytes.  (Infinity-Cache hits are counted by these counters, not excluded.)
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+import statistics
+
+CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output
+    "spmv_bj": "void vtk::k_spmv<double, false, 2, 8>",
+    "spmv": "void vtk::k_spmv<double, false, 0, 1>",
+    "spmv_resid": "void vtk::k_spmv<double, false, 1, 1>",
+    "mgs": "vtk::k_mgs(",
+    "tail": "vtk::k_tail(",
+    "xupdate": "vtk::k_xupdate(",
+    "bj_apply": "vtk::k_bj_apply(",
+    "scale0": "vtk::k_scale0(",
+}
+
+
+def load(path):
+    d = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", required=True)
+    ap.add_argument("--src", default="gpurun_out")
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    src = os.path.join(root, a.src)
+    ks = os.path.join(src, "prof", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(prof, f"{a.round}_kernel_stats.csv"))
+    fetch = load(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
+    write = load(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    out = {"_how": ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                    "'python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5'; "
+                    "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
+                    "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)"),
+           "note": a.note, "kernels": {}}
+    for cls, prefix in CLASSES.items():
+        fk = [v for k, vs in fetch.items() if k.startswith(prefix) for v in vs]
+        wk = [v for k, vs in write.items() if k.startswith(prefix) for v in vs]
+        if not fk:
+            continue
+        f_kib, w_kib = statistics.mean(fk), statistics.mean(wk) if wk else 0.0
+        out["kernels"][cls] = {"dispatches": len(fk), "fetch_kib": f_kib, "write_kib": w_kib,
+                               "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024}
+    dst = os.path.join(prof, f"{a.round}_pmc_traffic.json")
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", dst)
+    for k, v in out["kernels"].items():
+        print(f"  {k:12s} {v['dispatches']:6d} dispatches  {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch")
+
+
+if __name__ == "__main__":
+    main()

@@ -71,12 +71,65 @@ int dalloc(vtk_ctx *c, DBuf &b, size_t bytes) {
 
 int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
 
+// ---- kernel profile: HIP events around each launch on the context stream ------------------
+hipEvent_t prof_event(vtk_ctx *c) {
+    if (!c->prof_pool.empty()) { hipEvent_t e = c->prof_pool.back(); c->prof_pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+int prof_class(vtk_ctx *c, const char *name) {
+    for (size_t i = 0; i < c->prof_acc.size(); ++i) if (c->prof_acc[i].name == name) return (int)i;
+    c->prof_acc.push_back(vtk_ctx::ProfAcc{name});
+    return (int)c->prof_acc.size() - 1;
+}
+
+// brackets one launch: start event at construction, stop event at scope exit
+struct Prof {
+    vtk_ctx *c;
+    size_t idx = (size_t)-1;
+    Prof(vtk_ctx *c_, const char *name, int col, double bytes) : c(c_) {
+        if (!c->prof_on) return;
+        vtk_ctx::ProfPending p{prof_class(c, name), col, bytes, prof_event(c), prof_event(c)};
+        (void)hipEventRecord(p.e0, c->stream);
+        c->prof_pending.push_back(p);
+        idx = c->prof_pending.size() - 1;
+    }
+    ~Prof() { if (idx != (size_t)-1) (void)hipEventRecord(c->prof_pending[idx].e1, c->stream); }
+};
+
+// fold pending launches into the per-class counters; launches of columns after the cycle's
+// stop column (no-op kernels) are dropped
+void prof_flush(vtk_ctx *c, int last_col = 1 << 30) {
+    if (c->prof_pending.empty()) return;
+    (void)hipStreamSynchronize(c->stream);
+    for (auto &p : c->prof_pending) {
+        if (p.col <= last_col) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, p.e0, p.e1) == hipSuccess) {
+                auto &a = c->prof_acc[p.cls];
+                a.launches += 1;
+                a.seconds += ms * 1e-3;
+                a.bytes += p.bytes;
+            }
+        }
+        c->prof_pool.push_back(p.e0);
+        c->prof_pool.push_back(p.e1);
+    }
+    c->prof_pending.clear();
+}
+
+// reducing-kernel grid: a function of the local size on one GPU; GMAX on every rank when
+// world > 1 (equal partial-vector lengths for the in-place all-reduce)
+int grid_for(vtk_ctx *c, int g) { return c->world > 1 ? GMAX : g; }
+
 int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tiles &t) {
     std::vector<int32_t> rows;
     build_tiles(indptr, align, rows, t.has_long, t.aligned);
     t.ntiles = (int)rows.size() - 1;
     t.align = align;
-    t.grid = std::max(1, std::min(t.ntiles, GMAX));
+    t.grid = grid_for(c, std::max(1, std::min(t.ntiles, GMAX)));
     if (t.d_row) (void)hipFree(t.d_row);
     t.d_row = nullptr;
     HIPCHK(c, hipMalloc(&t.d_row, rows.size() * sizeof(int32_t)));
@@ -141,21 +194,22 @@ int comm_allgather_i64(vtk_ctx *c, const int64_t *send, int64_t *recv, int64_t c
     return VTK_OK;
 }
 
-// partial sums -> consumer view; across ranks: finalise to a scalar slot + all-reduce
+// partial sums -> consumer view.  Across ranks every reducing kernel runs on exactly GMAX
+// workgroups (grid_for), so the partial vectors have the same length on every rank and are
+// all-reduced in place: consumers then sum them exactly as on one GPU, with no extra kernel.
 Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
     rc = VTK_OK;
-    if (c->world == 1) return Red{part, cnt};
-    static thread_local int slot = 0;
-    double *dst = c->d_scal + (slot++ & 255);
-    hipError_t e = launch_finalize(Red{part, cnt}, dst, 0, c->stream);
-    if (e != hipSuccess) { rc = fail(c, VTK_ERR_HIP, hipGetErrorString(e)); return Red{dst, 1}; }
-    rc = comm_allreduce(c, dst, 1);
-    return Red{dst, 1};
+    if (c->world > 1) {
+        Prof pf(c, "allreduce", -1, 8.0 * cnt);
+        rc = comm_allreduce(c, part, cnt);
+    }
+    return Red{part, cnt};
 }
 
 int halo_exchange(vtk_csr *A, const double *x) {
     vtk_ctx *c = A->ctx;
     if (c->world == 1) return VTK_OK;
+    Prof pf(c, "halo", -1, 16.0 * A->n_send + 8.0 * A->n_halo);
     HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
     return comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble, sizeof(double));
 }
@@ -281,15 +335,24 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
     vtk_csr *A = s.A;
     TRY(halo_exchange(A, v));
     const double *v0 = s.V;
+    const double n8 = 8.0 * s.n;
+    const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (s.n + 1);
+    const double b_inv = s.M ? 8.0 * s.M->bs * s.n : 0.0;
     int cnt;
     if (!s.M) {
+        Prof pf(c, "spmv_w", col, b_csr + 3 * n8);
         HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PREC, w, nullptr, nullptr, 0, v0, s.part[0], s.part[1], stop, col, c->stream));
         cnt = A->tiles.grid;
     } else if (s.M->fused) {
+        Prof pf(c, "spmv_bj", col, b_csr + b_inv + 3 * n8);   // x, v0, w + CSR + BJ rows
         HIPCHK(c, launch_spmv(spmv_in(A, &s.M->tiles, v), EPI_PREC, w, nullptr, s.M->d_inv, s.M->bs, v0, s.part[0], s.part[1], stop, col, c->stream));
         cnt = s.M->tiles.grid;
     } else {
-        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, nullptr, 0, nullptr, nullptr, nullptr, stop, col, c->stream));
+        {
+            Prof pf(c, "spmv", col, b_csr + 2 * n8);
+            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, nullptr, 0, nullptr, nullptr, nullptr, stop, col, c->stream));
+        }
+        Prof pf(c, "bj_apply", col, b_inv + 3 * n8);
         HIPCHK(c, launch_bj_apply(s.M->d_inv, s.M->bs, s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
         cnt = s.G;
     }
@@ -311,12 +374,14 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     if (restart > MAX_RESTART) return fail(c, VTK_ERR_ARG, "restart exceeds MAX_RESTART");
     if (restart < 1) return fail(c, VTK_ERR_ARG, "empty system");
     const int m = restart;
-    Solver s{A, M, c, n, round_up(std::max<int64_t>(n, 1), 64), m, vector_grid(n), nullptr, nullptr,
+    Solver s{A, M, c, n, round_up(std::max<int64_t>(n, 1), 64), m, grid_for(c, vector_grid(n)), nullptr, nullptr,
              nullptr, nullptr, nullptr, nullptr, nullptr, {c->d_part, c->d_part + GMAX, c->d_part + 2 * GMAX, c->d_part + 3 * GMAX}};
     // workspace: V[(m+1) x ld] | w | tmp | r | H[m x (m+1)] | S[m+1] | giv[2m]  (doubles)
     const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
+    prof_flush(c);
+    for (auto e : c->prof_pool) (void)hipEventDestroy(e);
         c->ws = nullptr;
         c->ws_bytes = 0;
         HIPCHK(c, hipMalloc(&c->ws, nd * sizeof(double)));
@@ -337,18 +402,24 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     hs->stop_col = BIG_COL;
     HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(GmresState), hipMemcpyHostToDevice, c->stream));
     int rc;
+    const double n8 = 8.0 * n;
+    const double b_spmv = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 2 * n8;
+    const double b_pc = M ? 8.0 * M->bs * n + 2 * n8 : 2 * n8;
     // ||b|| and ||M b|| (iterative.py:708, :714)
-    HIPCHK(c, launch_dot(b, nullptr, n, s.part[0], s.G, c->stream));
+    { Prof pf(c, "dot", -1, n8);
+      HIPCHK(c, launch_dot(b, nullptr, n, s.part[0], s.G, c->stream)); }
     Red rb = reduce(c, s.part[0], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rb, &ds->scal[0], 1, c->stream));
-    HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream));
+    { Prof pf(c, "bj_apply", -1, b_pc);
+      HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream)); }
     Red rmb = reduce(c, s.part[1], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rmb, &ds->scal[1], 1, c->stream));
     // r = b - A x (iterative.py:737)
     TRY(halo_exchange(A, x));
-    HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream));
+    { Prof pf(c, "spmv_resid", -1, b_spmv + n8);
+      HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream)); }
     Red rr = reduce(c, s.part[2], A->tiles.grid, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rr, &ds->rnorm, 1, c->stream));
@@ -389,10 +460,12 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         // cycle start: v0 = M^-1 r / ||M^-1 r||, S = [tmp, 0, ...] (:742-748)
         hs->ptol = ptol;
         HIPCHK(c, hipMemcpyAsync(&ds->ptol, &hs->ptol, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream));
+        { Prof pf(c, "bj_apply", -1, b_pc);
+          HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
         Red rv = reduce(c, s.part[0], s.G, rc);
         TRY(rc);
-        HIPCHK(c, launch_scale0(rv, s.V, n, s.S, m, ds, s.G, c->stream));
+        { Prof pf(c, "scale0", -1, 2 * n8);
+          HIPCHK(c, launch_scale0(rv, s.V, n, s.S, m, ds, s.G, c->stream)); }
         const int *stop = &ds->stop_col;
         *mirror = BIG_COL;
         int enq = 0;
@@ -404,11 +477,13 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             for (int k = 0; k <= col; ++k) {
                 double *po = s.part[2 + (k & 1)];
                 const double *vn = k < col ? s.V + (size_t)(k + 1) * s.ld : nullptr;
-                HIPCHK(c, launch_mgs(cur, s.H + (size_t)col * (m + 1) + k, s.w, s.V + (size_t)k * s.ld, vn, n, po, s.G, stop, col, c->stream));
+                { Prof pf(c, "mgs", col, (vn ? 4 : 3) * n8);
+                  HIPCHK(c, launch_mgs(cur, s.H + (size_t)col * (m + 1) + k, s.w, s.V + (size_t)k * s.ld, vn, n, po, s.G, stop, col, c->stream)); }
                 cur = reduce(c, po, s.G, rc);
                 TRY(rc);
             }
-            HIPCHK(c, launch_tail(h0, cur, s.w, s.V + (size_t)(col + 1) * s.ld, n, col, m, s.H, s.S, s.giv, ds, c->d_stop, s.G, c->stream));
+            { Prof pf(c, "tail", col, 2 * n8);
+              HIPCHK(c, launch_tail(h0, cur, s.w, s.V + (size_t)(col + 1) * s.ld, n, col, m, s.H, s.S, s.giv, ds, c->d_stop, s.G, c->stream)); }
             HIPCHK(c, hipEventRecord(ev[col % (LOOKAHEAD + 1)], c->stream));
             enq = col + 1;
             if (col >= LOOKAHEAD) {
@@ -422,15 +497,22 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         }
         (void)enq;
         // x += y @ V[:col+1] (:799-814), r = b - A x, rnorm (:816-817)
-        HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream));
+        const size_t xup_idx = c->prof_pending.size();
+        { Prof pf(c, "xupdate", -1, 0.0);   // bytes set once the stop column is known
+          HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream)); }
         TRY(halo_exchange(A, x));
-        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream));
+        { Prof pf(c, "spmv_resid", -1, b_spmv + n8);
+          HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream)); }
         Red rr2 = reduce(c, s.part[2], A->tiles.grid, rc);
         TRY(rc);
         HIPCHK(c, launch_finalize(rr2, &ds->rnorm, 1, c->stream));
         HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         const int last = hs->stop_col < m ? hs->stop_col : m - 1;
+        if (c->prof_on) {
+            if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].bytes = n8 * (last + 1) + 2 * n8;
+            prof_flush(c, last);
+        }
         for (int j = 0; j <= last; ++j) st.bytes_moved += bytes_spmv + bytes_pc + 8.0 * n * (2 * j + 8);
         st.bytes_moved += bytes_spmv + 24.0 * n + bytes_pc + 24.0 * n + 8.0 * n * (last + 2);
         rnorm = hs->rnorm;
@@ -443,6 +525,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         else ptol_max_factor = std::min(1.0, 1.5 * ptol_max_factor);              // :833
         ptol = presid * std::min(ptol_max_factor, atol / rnorm);                    // :835
     }
+    prof_flush(c);
     st.inner_iters = hs->inner;
     st.presid = presid;
     st.rnorm = rnorm;
@@ -707,7 +790,11 @@ int vtk_spmv(vtk_csr *A, const double *x, double *y, int kind) {
     TRY(stage_in(c, x, A->n_local, kind, sx));
     TRY(stage_in(c, kind == VTK_PTR_DEVICE ? y : nullptr, A->n_local, kind, sy));
     TRY(halo_exchange(A, sx.d));
-    HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, sx.d), EPI_PLAIN, sy.d, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, c->stream));
+    {
+        Prof pf(c, "spmv", -1, (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (A->n_local + 1) + 16.0 * A->n_local);
+        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, sx.d), EPI_PLAIN, sy.d, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, c->stream));
+    }
+    if (c->prof_on) prof_flush(c);
     if (kind == VTK_PTR_HOST) {
         HIPCHK(c, hipMemcpyAsync(y, sy.d, A->n_local * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -764,7 +851,11 @@ int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
     Staged sr, sz;
     TRY(stage_in(c, r, n, kind, sr));
     TRY(stage_in(c, kind == VTK_PTR_DEVICE ? z : nullptr, n, kind, sz));
-    HIPCHK(c, launch_bj_apply(M->d_inv, M->bs, n, sr.d, sz.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0, c->stream));
+    {
+        Prof pf(c, "bj_apply", -1, 8.0 * M->bs * n + 16.0 * n);
+        HIPCHK(c, launch_bj_apply(M->d_inv, M->bs, n, sr.d, sz.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0, c->stream));
+    }
+    if (c->prof_on) prof_flush(c);
     if (kind == VTK_PTR_HOST) {
         HIPCHK(c, hipMemcpyAsync(z, sz.d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -784,6 +875,28 @@ int vtk_gmres_set_orth(vtk_ctx *c, int orth) {
     if (!c || (orth != VTK_ORTH_MGS && orth != VTK_ORTH_CGS2)) return VTK_ERR_ARG;
     if (orth == VTK_ORTH_CGS2) return fail(c, VTK_ERR_ARG, "CGS2 not available in this build");
     c->orth = orth;
+    return VTK_OK;
+}
+
+int vtk_profile_enable(vtk_ctx *c, int on) {
+    if (!c) return VTK_ERR_ARG;
+    prof_flush(c);
+    c->prof_on = on != 0;
+    if (c->prof_on) c->prof_acc.clear();
+    return VTK_OK;
+}
+
+int vtk_profile_read(vtk_ctx *c, vtk_kernel_profile *out, int max_entries, int *n_entries) {
+    if (!c || !n_entries || (max_entries > 0 && !out)) return VTK_ERR_ARG;
+    prof_flush(c);
+    *n_entries = (int)c->prof_acc.size();
+    for (int i = 0; i < max_entries && i < (int)c->prof_acc.size(); ++i) {
+        const auto &a = c->prof_acc[i];
+        std::snprintf(out[i].name, sizeof(out[i].name), "%s", a.name.c_str());
+        out[i].launches = a.launches;
+        out[i].seconds = a.seconds;
+        out[i].bytes = a.bytes;
+    }
     return VTK_OK;
 }
 

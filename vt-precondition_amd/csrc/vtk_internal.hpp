@@ -68,6 +68,13 @@ struct vtk_ctx {
     int *d_stop = nullptr;                // device alias of h_stop
     void *ws = nullptr;                   // solver workspace (grow-only, reused across solves)
     size_t ws_bytes = 0;
+    // kernel profile (vtk_profile_enable)
+    struct ProfPending { int cls; int col; double bytes; hipEvent_t e0, e1; };
+    struct ProfAcc { std::string name; int64_t launches = 0; double seconds = 0, bytes = 0; };
+    bool prof_on = false;
+    std::vector<ProfPending> prof_pending;
+    std::vector<ProfAcc> prof_acc;
+    std::vector<hipEvent_t> prof_pool;
 };
 
 struct vtk_csr {

@@ -242,7 +242,7 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
 hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
                        int bs, const double *v0, double *part0, double *part1,
                        const int *stop_col, int col, hipStream_t s) {
-    if (in.tiles->ntiles == 0) return hipSuccess;
+    // ntiles == 0 still launches: reducing epilogues must write their (zero) partials
     const bool halo = in.halo != nullptr;
     if (in.fp32) {
         return halo ? spmv_dispatch<float, true>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s)
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(NT) void k_bj_apply(const double *__restrict__ inv,
 hipError_t launch_bj_apply(const double *inv, int bs, int64_t n, const double *r, double *z,
                            const double *v0, double *part0, double *part1, int grid,
                            const int *stop_col, int col, hipStream_t s) {
-    if (n == 0) return hipSuccess;
+    if (n == 0 && part0 == nullptr) return hipSuccess;
     hipLaunchKernelGGL(k_bj_apply, dim3(grid), dim3(NT), 0, s, inv, bs, n, r, z, v0, part0, part1,
                        stop_col, col);
     return hipGetLastError();

@@ -113,6 +113,24 @@ class Context:
         from .comm import init_host
         return init_host(self, rank, world, group)
 
+    def profile(self, on: bool = True):
+        """Enable (and clear) / disable the per-kernel-class event profile."""
+        check(lib().vtk_profile_enable(self._h, int(bool(on))), self._h)
+
+    def profile_read(self) -> dict:
+        """{class: {launches, seconds, bytes, avg_us, gbs}} from the event profile."""
+        n = C.c_int()
+        check(lib().vtk_profile_read(self._h, None, 0, C.byref(n)), self._h)
+        arr = (_abi.KernelProfile * max(n.value, 1))()
+        check(lib().vtk_profile_read(self._h, arr, n.value, C.byref(n)), self._h)
+        out = {}
+        for e in arr[:n.value]:
+            if e.launches:
+                out[e.name.decode()] = {"launches": e.launches, "seconds": e.seconds, "bytes": e.bytes,
+                                        "avg_us": e.seconds / e.launches * 1e6,
+                                        "gbs": e.bytes / e.seconds / 1e9 if e.seconds > 0 else 0.0}
+        return out
+
     def set_orth(self, orth: int):
         check(lib().vtk_gmres_set_orth(self._h, int(orth)), self._h)
 

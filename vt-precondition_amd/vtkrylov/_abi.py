@@ -82,7 +82,14 @@ PROTOTYPES = {
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
                             C.POINTER(C.c_int), C.POINTER(Stats)]),
     "vtk_gmres_set_orth": (C.c_int, [P, C.c_int]),
+    "vtk_profile_enable": (C.c_int, [P, C.c_int]),
+    "vtk_profile_read": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_int)]),
 }
+
+
+class KernelProfile(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("seconds", C.c_double),
+                ("bytes", C.c_double)]
 
 _lib = None
 
