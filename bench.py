@@ -204,6 +204,42 @@ def main():
     dk = kprof[dom]
 
     ms = elapsed / args.steps * 1e3
+    out = {
+        "metric": "precond-GMRES iters/sec + CSR SpMV achieved-HBM-GB/s, 1/2/4/8 MI355X",
+        "value": iters / elapsed,
+        "unit": "iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if not fp32 else "f32-values/f64",
+        "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
+        "config": {"workload": f"{args.config}: GMRES({args.restart})+BJ({args.bs}) to rtol={args.rtol}, "
+                               f"n={n_glob}, row-sharded over {world} GPU(s)",
+                   "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
+                   "bs": args.bs, "rtol": args.rtol, "parallelism": f"row-slab x{world}",
+                   "comm": args.comm if world > 1 else None},
+        "inner_iters_per_solve": iters / args.steps,
+        "info": infos,
+        "true_rel_residual": rel_res,
+        "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B},
+        "roofline": {"kernel": dom, "bound": "hbm", "achieved": dk["gbs"], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": dk["gbs"] / HBM_PEAK_GBS,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],
+                     "avg_us": dk["avg_us"], "launches": dk["launches"],
+                     "share_of_solve": dk["seconds"] / tot_s},
+        "roofline_spmv": {"kernel": "spmv (plain CSR-stream, vtk_spmv)", "bound": "hbm",
+                          "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": spmv_gbs / HBM_PEAK_GBS, "traffic": pmc_traffic("spmv", args.config, world),
+                          "algorithmic_bytes_per_launch": B},
+        "kernels": {k: {"avg_us": round(v["avg_us"], 2), "gbs": round(v["gbs"], 1),
+                        "launches": v["launches"], "share": round(v["seconds"] / tot_s, 4)}
+                    for k, v in sorted(kprof.items(), key=lambda kv: -kv[1]["seconds"])},
+        "cpu_baseline": None,
+    }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             A_host = A.download()
