@@ -1,0 +1,56 @@
+"""vtconfig/vtsetup entry layer: the reference's XML lookup conventions
+(ini_info.py:72-118) and the step object's fixed main() sequence."""
+import json
+
+import numpy as np
+import pytest
+
+from vtsetup.config import DEFAULT_XML, Etree, SolverConfig, parse_config_spec
+
+
+def test_lookup_conventions():
+    t = Etree(DEFAULT_XML)
+    assert t.get_node_value("solver/restart") == "20"
+    assert t.get_node_value("rtol") == "1e-8"            # .//attrib search, like the reference
+    phys = t.dict_walkData("operator/physics")
+    assert phys == {"vmax": "6.0", "E0": "0.5", "nu": "0.05", "alpha": "0.25", "cfl": "4.0"}
+    with pytest.raises(KeyError):
+        t.get_node_value("solver/nonexistent")
+
+
+def test_typed_config_and_overrides():
+    c = SolverConfig.load()
+    assert (c.config, c.dim, c.shape, c.fp32) == ("C3", 2, (25000, 800), False)
+    assert (c.rtol, c.atol, c.restart, c.block_size, c.seed) == (1e-8, 0.0, 20, 8, 0x5EED)
+    c4 = SolverConfig.load(config="C4")
+    assert (c4.dim, c4.shape, c4.fp32) == (4, (200, 125, 50, 40), True)
+    assert parse_config_spec("1:10000:f64") == (1, (10000,), False)
+    with pytest.raises(ValueError):
+        parse_config_spec("2:10x10x10:f64")
+    with pytest.raises(KeyError):
+        SolverConfig.load(config="C9")
+
+
+def test_configs_match_oracle_specs():
+    from oracle import twin
+    t = Etree(DEFAULT_XML)
+    for name, spec in t.dict_walkData("operator/configs").items():
+        dim, shape, fp32 = parse_config_spec(spec)
+        p = twin.CONFIGS[name]
+        assert (p.dim, tuple(p.shape), p.fp32) == (dim, shape, fp32), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["S2", "C1"])
+def test_step_main_runs_on_gpu(gpu, tmp_path, name):
+    from oracle import coracle, twin
+    from vtsetup.krylov_precondition import KrylovPrecondition
+    cfg = SolverConfig.load(config=name, report=str(tmp_path / "r.json"))
+    step = KrylovPrecondition(cfg, ctx=gpu)
+    res = step.main()
+    assert res["solve"]["info"] == 0
+    assert json.load(open(tmp_path / "r.json"))["solve"]["inner_iters"] == res["solve"]["inner_iters"]
+    p = twin.CONFIGS[name]
+    ip, ix, d = coracle.generate(p)
+    b = twin.rhs(p.n)
+    assert np.linalg.norm(b - coracle.spmv(ip, ix, d, step.x)) <= 1e-8 * np.linalg.norm(b)

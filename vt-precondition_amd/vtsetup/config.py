@@ -1,0 +1,95 @@
+"""vtconfig reader for the Krylov path.
+
+Keeps the reference's two lookup conventions (ini_info.py:72-118) so configuration reads the
+same way as the rest of VT-precondition:
+    Etree.get_node_value("solver/rtol")      -> stripped text of the first matching node
+    Etree.dict_walkData("operator/physics")  -> {child tag: stripped text}
+but the file is a parameter (not a hard-coded path) and is parsed once per Etree instance.
+``SolverConfig.load(path)`` turns it into typed values.
+"""
+from __future__ import annotations
+
+import os
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass
+
+DEFAULT_XML = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           "vtconfig", "vt_krylov_configuration.xml")
+
+
+class Etree:
+    def __init__(self, path: str = DEFAULT_XML):
+        self.path = path
+        self.root = ET.parse(path).getroot()
+
+    def _find(self, attrib: str):
+        node = self.root.find(f".//{attrib}")
+        if node is None:
+            raise KeyError(f"{attrib!r} not found in {self.path}")
+        return node
+
+    def get_node_value(self, attrib: str) -> str:
+        return (self._find(attrib).text or "").strip()
+
+    def dict_walkData(self, attrib: str) -> dict:
+        return {n.tag: (n.text or "").strip() for n in self._find(attrib)}
+
+
+def parse_config_spec(spec: str):
+    """'2:1250x800:f64' -> (dim, shape, fp32)"""
+    dim, shape, prec = spec.split(":")
+    shape = tuple(int(v) for v in shape.split("x"))
+    dim = int(dim)
+    if {1: 1, 2: 2, 4: 4}.get(dim) != len(shape):
+        raise ValueError(f"config {spec!r}: dim {dim} needs {dim} extents")
+    if prec not in ("f64", "f32"):
+        raise ValueError(f"config {spec!r}: precision must be f64 or f32")
+    return dim, shape, prec == "f32"
+
+
+@dataclass
+class SolverConfig:
+    config: str
+    dim: int
+    shape: tuple
+    fp32: bool
+    physics: dict
+    rtol: float
+    atol: float
+    restart: int
+    maxiter: int
+    orth: str
+    preconditioner: str
+    block_size: int
+    seed: int
+    device: int
+    report: str
+
+    @classmethod
+    def load(cls, path: str = DEFAULT_XML, **overrides) -> "SolverConfig":
+        t = Etree(path)
+        name = overrides.pop("config", None) or t.get_node_value("solver/config")
+        specs = t.dict_walkData("operator/configs")
+        if name not in specs:
+            raise KeyError(f"config {name!r} not in operator/configs ({sorted(specs)})")
+        dim, shape, fp32 = parse_config_spec(specs[name])
+        phys = {k: float(v) for k, v in t.dict_walkData("operator/physics").items()}
+        cfg = cls(config=name, dim=dim, shape=shape, fp32=fp32, physics=phys,
+                  rtol=float(t.get_node_value("solver/rtol")),
+                  atol=float(t.get_node_value("solver/atol")),
+                  restart=int(t.get_node_value("solver/restart")),
+                  maxiter=int(t.get_node_value("solver/maxiter")),
+                  orth=t.get_node_value("solver/orth").lower(),
+                  preconditioner=t.get_node_value("preconditioner/type").lower(),
+                  block_size=int(t.get_node_value("preconditioner/block_size")),
+                  seed=int(t.get_node_value("rhs/seed"), 0),
+                  device=int(t.get_node_value("run/device")),
+                  report=t.get_node_value("run/report"))
+        for k, v in overrides.items():
+            if v is not None:
+                setattr(cfg, k, v)
+        if cfg.preconditioner not in ("block_jacobi", "none"):
+            raise ValueError(f"unknown preconditioner {cfg.preconditioner!r}")
+        if cfg.orth not in ("mgs", "cgs2"):
+            raise ValueError(f"unknown orthogonalisation {cfg.orth!r}")
+        return cfg

@@ -1,0 +1,91 @@
+"""vtsetup entry for the preconditioned-Krylov path.
+
+Mirrors the reference's step-object convention — a class whose ``main()`` runs a fixed
+sequence (hypervisor.py:589-594: deploy -> network -> tools -> vms -> env) — with the
+solver's sequence: generate operator -> set up preconditioner -> solve -> report.  Errors
+surface as exceptions that ``test_main`` turns into a return code, as in
+vt_precondition.py:66-79.
+
+    python -m vtsetup.krylov_precondition [--config C1] [--xml path] [--report out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+
+
+class KrylovPrecondition:
+    def __init__(self, cfg, ctx=None):
+        self.cfg = cfg
+        self.ctx = ctx
+        self.A = self.M = self.b = self.x = None
+        self.result = {}
+
+    def generate_operator(self):
+        import vtkrylov as vk
+        c = self.cfg
+        self.ctx = self.ctx or vk.Context(c.device)
+        if c.orth == "cgs2":
+            self.ctx.set_orth(1)
+        p = vk.vlasov_params(c.dim, c.shape, fp32=c.fp32, **c.physics)
+        t = time.perf_counter()
+        self.A = vk.vlasov_operator(p, ctx=self.ctx)
+        self.result["operator"] = {"n": self.A.n_global, "nnz": self.A.nnz,
+                                   "t_assemble_s": time.perf_counter() - t}
+
+    def setup_preconditioner(self):
+        import vtkrylov as vk
+        t = time.perf_counter()
+        if self.cfg.preconditioner == "block_jacobi":
+            self.M = vk.block_jacobi(self.A, self.cfg.block_size)
+        self.result["preconditioner"] = {"type": self.cfg.preconditioner,
+                                         "block_size": self.cfg.block_size,
+                                         "t_setup_s": time.perf_counter() - t}
+
+    def solve(self):
+        import vtkrylov as vk
+        c = self.cfg
+        self.b = vk.rhs_splitmix(self.A.n_global, seed=c.seed)
+        self.x, info = vk.gmres(self.A, self.b, rtol=c.rtol, atol=c.atol, restart=c.restart,
+                                maxiter=c.maxiter or None, M=self.M)
+        st = vk.last_stats()
+        self.result["solve"] = {"info": info, "inner_iters": st.inner_iters,
+                                "restarts": st.restarts, "rnorm": st.rnorm, "bnorm": st.bnorm,
+                                "t_solve_s": st.t_solve,
+                                "iters_per_s": st.inner_iters / st.t_solve if st.t_solve else None}
+
+    def report(self):
+        self.result["config"] = self.cfg.config
+        if self.cfg.report:
+            with open(self.cfg.report, "w") as f:
+                json.dump(self.result, f, indent=1)
+        return self.result
+
+    def main(self):
+        self.generate_operator()
+        self.setup_preconditioner()
+        self.solve()
+        return self.report()
+
+
+def test_main(argv=None) -> int:
+    from .config import DEFAULT_XML, SolverConfig
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--xml", default=DEFAULT_XML)
+    ap.add_argument("--config")
+    ap.add_argument("--report")
+    a = ap.parse_args(argv)
+    try:
+        cfg = SolverConfig.load(a.xml, config=a.config, report=a.report)
+        res = KrylovPrecondition(cfg).main()
+        print(json.dumps(res))
+        return 0 if res["solve"]["info"] == 0 else 1
+    except Exception as e:   # vt_precondition.py:70-71 style: report and fail
+        print(f"vtsetup.krylov_precondition failed: {type(e).__name__}: {e}", file=sys.stderr)
+        return 2
+
+
+if __name__ == "__main__":
+    sys.exit(test_main())
