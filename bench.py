@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--spmv-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-inner", type=int, default=20)
+    ap.add_argument("--orth", default="mgs", choices=["mgs", "dcgs2"],
+                    help="orthogonalisation: mgs (SciPy's sequence) or dcgs2 (one reduction per step)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     args = ap.parse_args()
@@ -123,6 +125,7 @@ def main():
             vkcomm.init_rccl(ctx, rank, world)
         else:
             vkcomm.init_host(ctx, rank, world)
+    ctx.set_orth(vk._abi.ORTH_DCGS2 if args.orth == "dcgs2" else vk._abi.ORTH_MGS)
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
 
@@ -217,10 +220,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f64" if not fp32 else "f32-values/f64",
         "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
-        "config": {"workload": f"{args.config}: GMRES({args.restart})+BJ({args.bs}) to rtol={args.rtol}, "
+        "config": {"workload": f"{args.config}: GMRES({args.restart}, {args.orth})+BJ({args.bs}) to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "bs": args.bs, "rtol": args.rtol, "parallelism": f"row-slab x{world}",
+                   "bs": args.bs, "rtol": args.rtol, "orth": args.orth, "parallelism": f"row-slab x{world}",
                    "comm": args.comm if world > 1 else None},
         "inner_iters_per_solve": iters / args.steps,
         "info": infos,

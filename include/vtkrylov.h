@@ -54,8 +54,11 @@ typedef enum {
 typedef enum { VTK_PTR_HOST = 0, VTK_PTR_DEVICE = 1 } vtk_ptr_kind;
 
 typedef enum {
-    VTK_ORTH_MGS = 0,   /* modified Gram-Schmidt, SciPy's order (iterative.py:755-759)       */
-    VTK_ORTH_CGS2 = 1   /* classical GS + one re-orthogonalisation: 2 reductions per step   */
+    VTK_ORTH_MGS = 0,   /* modified Gram-Schmidt, SciPy's sequence (iterative.py:755-759):
+                           j+2 dependent reductions per Arnoldi step (default)              */
+    VTK_ORTH_DCGS2 = 1  /* delayed classical GS with re-orthogonalisation: ONE reduction and
+                           two passes over the basis per step; restart <= 32; the stop test of
+                           column j runs one step later (one extra SpMV per cycle)          */
 } vtk_orth;
 
 /* Synthetic Vlasov operator parameters. */

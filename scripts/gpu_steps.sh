@@ -24,6 +24,7 @@ for s in "$@"; do
         testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         bench) step bench 600 python bench.py ;;
         benchq) step benchq 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        benchdc) step benchdc 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth dcgs2 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         multirank) step multirank 900 python -m pytest tests/test_gpu_multirank.py -m gpu -x -q -p no:cacheprovider ;;
         bench2host) step bench2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --comm host --config C1 --steps 1 --warmup 1 --spmv-reps 3 ;;

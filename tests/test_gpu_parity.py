@@ -163,6 +163,15 @@ def test_bj_singular_block_raises(gpu, vk_lib):
         vk.block_jacobi(A, 8)
 
 
+@pytest.fixture(params=["mgs", "dcgs2"])
+def orth(request, gpu, vk_lib):
+    """Run a solver test with each orthogonalisation scheme; both must meet the same bars
+    against SciPy's MGS (same info, inner iterations +-1, x within tolerance)."""
+    gpu.set_orth({"mgs": vk_lib._abi.ORTH_MGS, "dcgs2": vk_lib._abi.ORTH_DCGS2}[request.param])
+    yield request.param
+    gpu.set_orth(vk_lib._abi.ORTH_MGS)
+
+
 def _check_solve(xg, info, st, ref_x, ref_info, ref_iters, tol=1e-9):
     assert info == ref_info
     assert abs(st.inner_iters - ref_iters) <= 1, (st.inner_iters, ref_iters)
@@ -171,7 +180,7 @@ def _check_solve(xg, info, st, ref_x, ref_info, ref_iters, tol=1e-9):
 
 
 @pytest.mark.parametrize("name", SMALL)
-def test_gmres_vs_oracle_and_scipy(ops, golden, name):
+def test_gmres_vs_oracle_and_scipy(ops, golden, name, orth):
     import vtkrylov as vk
     p, A, (ip, ix, d) = ops[name]
     M = vk.block_jacobi(A, 8)
@@ -187,7 +196,7 @@ def test_gmres_vs_oracle_and_scipy(ops, golden, name):
 
 
 @pytest.mark.parametrize("case", ["noprec", "x0", "restart5_maxiter3", "bzero", "atol", "restart40"])
-def test_gmres_edge_cases(ops, golden, case):
+def test_gmres_edge_cases(ops, golden, case, orth):
     import vtkrylov as vk
     p, A, (ip, ix, d) = ops["S2"]
     b = twin.rhs(p.n)
@@ -200,6 +209,10 @@ def test_gmres_edge_cases(ops, golden, case):
           "restart40": dict(M=M, rtol=1e-9, restart=40)}[case]
     if case == "bzero":
         b = np.zeros(p.n)
+    if orth == "dcgs2" and case == "restart40":   # DCGS2 is limited to restart <= 32: explicit
+        with pytest.raises(ValueError):
+            vk.gmres(A, b, **kw)
+        return
     xg, info = vk.gmres(A, b, **kw)
     st = vk.last_stats()
     meta = golden[f"edge/{case}/meta"]
@@ -211,7 +224,7 @@ def test_gmres_edge_cases(ops, golden, case):
     _check_solve(xg, info, st, gx, int(meta[0]), int(meta[1]), tol=1e-8)
 
 
-def test_gmres_ragged_generic_bs(gpu, vk_lib, golden):
+def test_gmres_ragged_generic_bs(gpu, vk_lib, golden, orth):
     vk = vk_lib
     ip, ix, d = golden["ragged/indptr"], golden["ragged/indices"], golden["ragged/data"]
     n = ip.shape[0] - 1
@@ -224,7 +237,7 @@ def test_gmres_ragged_generic_bs(gpu, vk_lib, golden):
     _check_solve(xg, info, st, golden["ragged/gmres_x"], int(meta[0]), int(meta[1]), tol=1e-8)
 
 
-def test_gmres_c1_vs_scipy_summary(ops, golden_large):
+def test_gmres_c1_vs_scipy_summary(ops, golden_large, orth):
     import vtkrylov as vk
     p, A, (ip, ix, d) = ops["C1"]
     M = vk.block_jacobi(A, 8)
@@ -235,12 +248,13 @@ def test_gmres_c1_vs_scipy_summary(ops, golden_large):
     assert info == g["info"] == 0
     assert abs(st.inner_iters - g["inner_iters"]) <= 1
     assert np.linalg.norm(xg) == pytest.approx(g["x_norm2"], rel=1e-9)
+    assert st.orth == (0 if orth == "mgs" else 1)
     np.testing.assert_allclose(xg[:8], g["x_first8"], rtol=1e-8)
     res = np.linalg.norm(b - coracle.spmv(ip, ix, d, xg))
     assert res <= 1e-8 * g["b_norm2"]
 
 
-def test_gmres_device_tensors(ops):
+def test_gmres_device_tensors(ops, orth):
     import torch
 
     import vtkrylov as vk
@@ -257,7 +271,7 @@ def test_gmres_device_tensors(ops):
 
 
 @pytest.mark.slow
-def test_gmres_c3_full_size(gpu, vk_lib):
+def test_gmres_c3_full_size(gpu, vk_lib, orth):
     """C3 (20M rows): the bench workload.  Size-independent properties: convergence to
     rtol, the true residual recomputed on the host by the oracle SpMV, and repeatability."""
     vk = vk_lib

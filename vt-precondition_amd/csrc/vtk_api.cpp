@@ -327,14 +327,17 @@ struct Solver {
     int m, G;
     double *V, *w, *tmp, *r, *H, *S, *giv;
     double *part[4];
+    double *Hraw = nullptr, *dcpart = nullptr;   // DCGS2
+    DcCoef *cf = nullptr;
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
-int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0) {
+int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0,
+                   bool want_dots = true) {
     vtk_ctx *c = s.c;
     vtk_csr *A = s.A;
     TRY(halo_exchange(A, v));
-    const double *v0 = s.V;
+    const double *v0 = want_dots ? s.V : nullptr;
     const double n8 = 8.0 * s.n;
     const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (s.n + 1);
     const double b_inv = s.M ? 8.0 * s.M->bs * s.n : 0.0;
@@ -356,11 +359,53 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
         HIPCHK(c, launch_bj_apply(s.M->d_inv, s.M->bs, s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
         cnt = s.G;
     }
-    int rc;
+    int rc = VTK_OK;
+    if (!want_dots) return rc;
     h0 = reduce(c, s.part[0], cnt, rc);
     TRY(rc);
     d0 = reduce(c, s.part[1], cnt, rc);
     return rc;
+}
+
+// One restart cycle with DCGS2 (see vtk_kernels.hip, DCGS2 Arnoldi).  Step j's SpMV, dots,
+// finalize and scalar kernels are tagged with column j-1 (the column they finalise), its update
+// pass with column j.  After column m-1, a closing reduction finalises it.
+int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev) {
+    vtk_ctx *c = s.c;
+    GmresState *ds = c->d_state;
+    const int m = s.m;
+    const int64_t n = s.n;
+    const double n8 = 8.0 * n;
+    auto reduce_step = [&](int j, const double *w, int col) -> int {
+        { Prof pf(c, "dc_dots", col, n8 * (j + (w ? 2 : 1)));
+          HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, col, c->stream)); }
+        { Prof pf(c, "dc_finalize", col, 0.0);
+          HIPCHK(c, launch_dc_finalize(s.dcpart, s.G, j, w != nullptr, c->d_scal, stop, col, c->stream)); }
+        if (c->world > 1) {
+            Prof pf(c, "allreduce", col, 8.0 * DC_NQ);
+            TRY(comm_allreduce(c, c->d_scal, DC_NQ));
+        }
+        Prof pf(c, "dc_scalar", col, 0.0);
+        HIPCHK(c, launch_dc_scalar(c->d_scal, j, m, w == nullptr, s.Hraw, s.H, s.S, s.giv, s.cf, ds, c->d_stop, c->stream));
+        return VTK_OK;
+    };
+    bool broke = false;
+    for (int j = 0; j < m; ++j) {
+        Red h0, d0;
+        double *pj = s.V + (size_t)j * s.ld;
+        TRY(precond_matvec(s, pj, s.w, stop, j - 1, h0, d0, false));
+        TRY(reduce_step(j, s.w, j - 1));
+        { Prof pf(c, "dc_update", j, n8 * (j + 4));
+          HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, c->stream)); }
+        HIPCHK(c, hipEventRecord(ev[j % (LOOKAHEAD + 1)], c->stream));
+        if (j >= LOOKAHEAD) {
+            HIPCHK(c, hipEventSynchronize(ev[(j - LOOKAHEAD) % (LOOKAHEAD + 1)]));
+            // a stop of column cc is decided in step cc+1: act only when every rank has run it
+            if (*mirror <= j - LOOKAHEAD - 1) { broke = true; break; }
+        }
+    }
+    if (!broke) TRY(reduce_step(m, nullptr, m - 1));   // closing: finalise column m-1
+    return VTK_OK;
 }
 
 int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, double atol,
@@ -377,7 +422,10 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     Solver s{A, M, c, n, round_up(std::max<int64_t>(n, 1), 64), m, grid_for(c, vector_grid(n)), nullptr, nullptr,
              nullptr, nullptr, nullptr, nullptr, nullptr, {c->d_part, c->d_part + GMAX, c->d_part + 2 * GMAX, c->d_part + 3 * GMAX}};
     // workspace: V[(m+1) x ld] | w | tmp | r | H[m x (m+1)] | S[m+1] | giv[2m]  (doubles)
-    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64;
+    const bool dc = c->orth == VTK_ORTH_DCGS2;
+    if (dc && m > DC_MAXJ) return fail(c, VTK_ERR_ARG, "DCGS2 supports restart <= 32");
+    const size_t ndc = dc ? (size_t)(m + 1) * (m + 1) + sizeof(DcCoef) / 8 + 8 + (size_t)DC_NQ * GMAX : 0;
+    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
     prof_flush(c);
@@ -394,7 +442,14 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     s.r = wp; wp += s.ld;
     s.H = wp; wp += (size_t)m * (m + 1);
     s.S = wp; wp += m + 1;
-    s.giv = wp;
+    s.giv = wp; wp += 2 * m;
+    if (dc) {
+        wp = reinterpret_cast<double *>((reinterpret_cast<uintptr_t>(wp) + 63) & ~(uintptr_t)63);
+        s.dcpart = wp; wp += (size_t)DC_NQ * GMAX;
+        s.Hraw = wp; wp += (size_t)(m + 1) * (m + 1);
+        s.cf = reinterpret_cast<DcCoef *>(wp);
+        HIPCHK(c, hipMemsetAsync(s.Hraw, 0, (size_t)(m + 1) * (m + 1) * sizeof(double), c->stream));
+    }
     HIPCHK(c, hipMemsetAsync(s.H, 0, (size_t)m * (m + 1) * sizeof(double), c->stream));
     HIPCHK(c, hipMemsetAsync(s.giv, 0, (size_t)2 * m * sizeof(double), c->stream));
     GmresState *ds = c->d_state, *hs = c->h_state;
@@ -431,7 +486,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     vtk_stats st{};
     st.bnorm = bnrm2;
     st.atol_eff = atol;
-    st.orth = VTK_ORTH_MGS;
+    st.orth = c->orth;
     auto done = [&](int inf) {
         *info = inf;
         st.t_solve = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -469,6 +524,9 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         const int *stop = &ds->stop_col;
         *mirror = BIG_COL;
         int enq = 0;
+        if (dc) {
+            TRY(dcgs2_cycle(s, stop, mirror, ev));
+        } else
         for (int col = 0; col < m; ++col) {
             double *vcol = s.V + (size_t)col * s.ld;
             Red h0, d0;
@@ -872,8 +930,7 @@ void vtk_prec_destroy(vtk_prec *M) {
 }
 
 int vtk_gmres_set_orth(vtk_ctx *c, int orth) {
-    if (!c || (orth != VTK_ORTH_MGS && orth != VTK_ORTH_CGS2)) return VTK_ERR_ARG;
-    if (orth == VTK_ORTH_CGS2) return fail(c, VTK_ERR_ARG, "CGS2 not available in this build");
+    if (!c || (orth != VTK_ORTH_MGS && orth != VTK_ORTH_DCGS2)) return fail(c, VTK_ERR_ARG, "vtk_gmres_set_orth: unknown scheme");
     c->orth = orth;
     return VTK_OK;
 }

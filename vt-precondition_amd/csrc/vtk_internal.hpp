@@ -31,6 +31,19 @@ struct GmresState {
     long long inner;      // inner iterations, cumulative
 };
 
+// DCGS2 (delayed classical Gram-Schmidt with re-orthogonalisation, one reduction per Arnoldi
+// step): per-step coefficients produced by the scalar kernel for the update pass
+constexpr int DC_MAXJ = 32;          // restart <= 32 in this mode (4 waves x 8 vectors per lane)
+constexpr int DC_NQ = 2 * DC_MAXJ + 3;   // reduction slots: s[32] | z[32] | alpha beta gamma
+struct DcCoef {
+    double s[DC_MAXJ];        // re-orthogonalisation coefficients of the candidate p_j
+    double e[DC_MAXJ + 1];    // projection of w on [V_j, v_j]
+    double rinv;              // 1 / r_j  (r_j = ||p_j - V_j s||, Pythagorean)
+    double q;                 // 1 / (r_j * nu_{j+1})
+    double nu;                // tentative h_{j+1,j}
+    double h0[DC_MAXJ + 1];   // ||B v_c|| per column (breakdown test, iterative.py:766)
+};
+
 // a reduced scalar as seen by a consumer kernel: G partials (single GPU) or 1 value (after
 // the RCCL all-reduce).  Every consumer workgroup sums the partials in the same fixed order.
 struct Red {
@@ -165,6 +178,18 @@ hipError_t launch_exclusive_scan(const int32_t *in, int32_t *out, int64_t n, voi
                                  size_t *tmp_bytes, hipStream_t s);
 hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, int64_t n_local,
                              const int64_t *halo_cols, int64_t n_halo, hipStream_t s);
+
+// DCGS2: dots pass (s = V_j^T p_j, z = V_j^T w, alpha, beta, gamma; w == null: s, alpha only),
+// per-quantity finalize (one workgroup per quantity), single-lane scalar step, update pass.
+hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, int64_t n,
+                          double *part, int grid, const int *stop_col, int col, hipStream_t s);
+hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, double *scal,
+                              const int *stop_col, int col, hipStream_t s);
+hipError_t launch_dc_scalar(const double *scal, int j, int m, int closing, double *Hraw,
+                            double *H, double *S, double *giv, DcCoef *cf, GmresState *st,
+                            int *stop_map, hipStream_t s);
+hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
+                            const DcCoef *cf, int grid, const int *stop_col, hipStream_t s);
 
 int vector_grid(int64_t n);
 

@@ -788,6 +788,257 @@ hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, i
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// DCGS2 Arnoldi (one global reduction per step).  State entering step j: V_j = [v_0..v_{j-1}]
+// orthonormal, candidate p_j = V[j] (orthogonalised once, normalised by an estimate), raw
+// Hessenberg column j-1 tentative.  Step j: w = M^-1 A p_j (SpMV); ONE pass of dots
+// s = V_j^T p_j, z = V_j^T w, alpha = |p|^2, beta = p.w, gamma = |w|^2; the scalar step
+// re-orthogonalises p_j (v_j = (p_j - V_j s)/r, r = sqrt(alpha - s.s)), finalises column j-1
+// (h += nu s, h_{j,j-1} = nu r), runs SciPy's Givens/stop logic on it, and forms the tentative
+// column j (c' = (e - H_j s)/r, e = [z; (beta - s.z)/r]) and nu_{j+1} = sqrt(gamma - e.e)/r;
+// ONE update pass writes v_j and p_{j+1} = (w - [V_j v_j] e) / (r nu).  Derivation: DESIGN.md.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_dc_dots(const double *__restrict__ V, int64_t ld, int j,
+                                                const double *__restrict__ w, int64_t n, double *part,
+                                                const int *stop_col, int col) {
+    constexpr int KPW = DC_MAXJ / (NT / 64);   // basis vectors per wave
+    __shared__ double red[DC_NQ];
+    if (stopped(stop_col, col)) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double *p = V + (size_t)j * ld;
+    double as[KPW], az[KPW];
+#pragma unroll
+    for (int u = 0; u < KPW; ++u) { as[u] = 0.0; az[u] = 0.0; }
+    double aa = 0.0, ab = 0.0, ag = 0.0;
+    const int64_t stride = 2 * (int64_t)gridDim.x * 64;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * 64 + lane); i < n; i += stride) {
+        const bool two = i + 1 < n;
+        double2 pv, wv2;
+        if (two) {
+            pv = *reinterpret_cast<const double2 *>(p + i);
+            wv2 = w ? *reinterpret_cast<const double2 *>(w + i) : make_double2(0.0, 0.0);
+        } else {
+            pv = make_double2(p[i], 0.0);
+            wv2 = make_double2(w ? w[i] : 0.0, 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < KPW; ++u) {
+            const int k = wv + u * (NT / 64);
+            if (k < j) {
+                const double *vk = V + (size_t)k * ld + i;
+                const double2 v = two ? *reinterpret_cast<const double2 *>(vk) : make_double2(vk[0], 0.0);
+                as[u] += v.x * pv.x;
+                as[u] += v.y * pv.y;
+                if (w) {
+                    az[u] += v.x * wv2.x;
+                    az[u] += v.y * wv2.y;
+                }
+            }
+        }
+        if (wv == 0) {
+            aa += pv.x * pv.x;
+            aa += pv.y * pv.y;
+            if (w) {
+                ab += pv.x * wv2.x;
+                ab += pv.y * wv2.y;
+                ag += wv2.x * wv2.x;
+                ag += wv2.y * wv2.y;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < KPW; ++u) {
+        const int k = wv + u * (NT / 64);
+        const double ts = wave_sum(as[u]);
+        const double tz = wave_sum(az[u]);
+        if (lane == 0 && k < j) { red[k] = ts; red[DC_MAXJ + k] = tz; }
+    }
+    {
+        const double t0 = wave_sum(aa), t1 = wave_sum(ab), t2 = wave_sum(ag);
+        if (wv == 0 && lane == 0) { red[2 * DC_MAXJ] = t0; red[2 * DC_MAXJ + 1] = t1; red[2 * DC_MAXJ + 2] = t2; }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < DC_NQ; q += NT) {
+        const bool used = q < j || (q >= DC_MAXJ && q < DC_MAXJ + j && w) || q == 2 * DC_MAXJ ||
+                          (w && q > 2 * DC_MAXJ);
+        if (used) part[(size_t)q * GMAX + blockIdx.x] = red[q];
+    }
+}
+
+hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, int64_t n, double *part,
+                          int grid, const int *stop_col, int col, hipStream_t s) {
+    if (j > DC_MAXJ) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_dc_dots, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, part, stop_col, col);
+    return hipGetLastError();
+}
+
+// one workgroup per used quantity: scal[q] = sum of its partials (fixed order)
+__global__ __launch_bounds__(NT) void k_dc_finalize(const double *part, int cnt, int j, int with_w,
+                                                    double *scal, const int *stop_col, int col) {
+    __shared__ double red[NT / 64];
+    if (stopped(stop_col, col)) return;
+    const int b = blockIdx.x;
+    int q;
+    if (b < j) q = b;
+    else if (with_w && b < 2 * j) q = DC_MAXJ + (b - j);
+    else q = 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < cnt; i += NT) acc += part[(size_t)q * GMAX + i];
+    const double t = block_sum(acc, red);
+    if (threadIdx.x == 0) scal[q] = t;
+}
+
+hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, double *scal,
+                              const int *stop_col, int col, hipStream_t s) {
+    const int nblk = with_w ? 2 * j + 3 : j + 1;
+    hipLaunchKernelGGL(k_dc_finalize, dim3(nblk), dim3(NT), 0, s, part, cnt, j, with_w, scal, stop_col, col);
+    return hipGetLastError();
+}
+
+// single lane: re-orthogonalisation scalars, column j-1 finalisation + SciPy's Givens/stop
+// logic (iterative.py:761-794), tentative column j and the update-pass coefficients
+__global__ void k_dc_scalar(const double *scal, int j, int m, int closing, double *Hraw, double *H,
+                            double *S, double *giv, DcCoef *cf, GmresState *st, int *stop_map) {
+    if (threadIdx.x != 0 || st->stop_col < j - 1) return;
+    const double *sv = scal, *zv = scal + DC_MAXJ;
+    const double alpha = scal[2 * DC_MAXJ], beta = scal[2 * DC_MAXJ + 1], gamma = scal[2 * DC_MAXJ + 2];
+    const int M1 = m + 1;
+    double r = 1.0;
+    if (j >= 1) {
+        double ss = 0.0;
+        for (int k = 0; k < j; ++k) ss += sv[k] * sv[k];
+        const double r2 = alpha - ss;
+        r = __builtin_sqrt(r2 > 0.0 ? r2 : alpha);
+        const int c = j - 1;
+        double *hr = Hraw + (size_t)c * M1;
+        const double nu = cf->nu;
+        for (int k = 0; k < j; ++k) hr[k] = hr[k] + nu * sv[k];
+        hr[j] = nu * r;
+        double *hc = H + (size_t)c * M1;
+        for (int k = 0; k <= j; ++k) hc[k] = hr[k];
+        const bool brk = hc[j] <= DBL_EPSILON * cf->h0[c];
+        if (brk) hc[j] = 0.0;
+        for (int k = 0; k < c; ++k) {
+            const double cg = giv[2 * k], sg = giv[2 * k + 1];
+            const double n0 = hc[k], n1 = hc[k + 1];
+            hc[k] = cg * n0 + sg * n1;
+            hc[k + 1] = -sg * n0 + cg * n1;
+        }
+        double cg, sg, mag;
+        d_lartg(hc[c], hc[c + 1], cg, sg, mag);
+        giv[2 * c] = cg;
+        giv[2 * c + 1] = sg;
+        hc[c] = mag;
+        hc[c + 1] = 0.0;
+        const double t = -sg * S[c];
+        S[c] = cg * S[c];
+        S[c + 1] = t;
+        const double presid = __builtin_fabs(t);
+        st->presid = presid;
+        st->inner += 1;
+        if (presid <= st->ptol || brk || closing) {
+            if (presid <= st->ptol || brk) {
+                st->breakdown = brk ? 1 : 0;
+                st->stop_col = c;
+                if (stop_map) __hip_atomic_store(stop_map, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
+    }
+    // tentative column j
+    cf->rinv = 1.0 / r;
+    for (int k = 0; k < j; ++k) cf->s[k] = sv[k];
+    double sz = 0.0;
+    for (int k = 0; k < j; ++k) sz += sv[k] * zv[k];
+    double ee = 0.0;
+    double *hj = Hraw + (size_t)j * M1;
+    for (int k = 0; k <= j; ++k) {
+        const double e = k < j ? zv[k] : (beta - sz) / r;
+        cf->e[k] = e;
+        ee += e * e;
+        double g = 0.0;   // (H_j s)_k over the final raw columns i < j (row k nonzero for i >= k-1)
+        for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) g += Hraw[(size_t)i * M1 + k] * sv[i];
+        hj[k] = (e - g) / r;
+    }
+    const double gn = __builtin_sqrt(gamma) / r;
+    const double nu2 = gamma - ee;
+    double nu = nu2 > 0.0 ? __builtin_sqrt(nu2) / r : 0.0;
+    if (!(nu > 1e-8 * gn)) nu = gn > 0.0 ? gn : 1.0;   // cancellation: r of the next step corrects
+    cf->nu = nu;
+    cf->h0[j] = gn;
+    cf->q = 1.0 / (r * nu);
+}
+
+hipError_t launch_dc_scalar(const double *scal, int j, int m, int closing, double *Hraw, double *H,
+                            double *S, double *giv, DcCoef *cf, GmresState *st, int *stop_map,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_dc_scalar, dim3(1), dim3(64), 0, s, scal, j, m, closing, Hraw, H, S, giv, cf, st,
+                       stop_map);
+    return hipGetLastError();
+}
+
+// v_j = (p_j - sum_k s_k v_k) / r  (in place, j >= 1);  p_{j+1} = (w - sum_k e_k v_k - e_j v_j) * q
+__global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_t ld, int j,
+                                                  const double *__restrict__ w, int64_t n,
+                                                  const DcCoef *cf, const int *stop_col) {
+    __shared__ double cs[DC_MAXJ], ce[DC_MAXJ + 1];
+    __shared__ double rinv_s, q_s;
+    if (stopped(stop_col, j)) return;
+    for (int k = threadIdx.x; k <= j; k += NT) {
+        if (k < j) cs[k] = cf->s[k];
+        ce[k] = cf->e[k];
+    }
+    if (threadIdx.x == 0) { rinv_s = cf->rinv; q_s = cf->q; }
+    __syncthreads();
+    const double rinv = rinv_s, q = q_s, ej = ce[j];
+    double *pj = V + (size_t)j * ld;
+    double *pn = V + (size_t)(j + 1) * ld;
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            const double2 p = *reinterpret_cast<const double2 *>(pj + i);
+            double2 a = p, t = *reinterpret_cast<const double2 *>(w + i);
+            for (int k = 0; k < j; ++k) {
+                const d2v v = ldnt2(V + (size_t)k * ld + i);
+                const double sk = cs[k], ek = ce[k];
+                a.x = a.x - sk * v.x;
+                a.y = a.y - sk * v.y;
+                t.x = t.x - ek * v.x;
+                t.y = t.y - ek * v.y;
+            }
+            double2 vj = p;
+            if (j >= 1) {
+                vj.x = a.x * rinv;
+                vj.y = a.y * rinv;
+                *reinterpret_cast<double2 *>(pj + i) = vj;
+            }
+            t.x = t.x - ej * vj.x;
+            t.y = t.y - ej * vj.y;
+            t.x = t.x * q;
+            t.y = t.y * q;
+            *reinterpret_cast<double2 *>(pn + i) = t;
+        } else {
+            const double p = pj[i];
+            double a = p, t = w[i];
+            for (int k = 0; k < j; ++k) {
+                const double v = V[(size_t)k * ld + i];
+                a = a - cs[k] * v;
+                t = t - ce[k] * v;
+            }
+            double vj = p;
+            if (j >= 1) { vj = a * rinv; pj[i] = vj; }
+            t = t - ej * vj;
+            pn[i] = t * q;
+        }
+    }
+}
+
+hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n, const DcCoef *cf,
+                            int grid, const int *stop_col, hipStream_t s) {
+    hipLaunchKernelGGL(k_dc_update, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, stop_col);
+    return hipGetLastError();
+}
+
 int vector_grid(int64_t n) {
     int64_t g = (n + 2 * NT - 1) / (2 * NT);
     if (g < 1) g = 1;

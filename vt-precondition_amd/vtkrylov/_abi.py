@@ -26,7 +26,7 @@ PTR_HOST = 0
 PTR_DEVICE = 1
 
 ORTH_MGS = 0
-ORTH_CGS2 = 1
+ORTH_DCGS2 = 1
 
 
 class VlasovParams(C.Structure):
