@@ -96,8 +96,9 @@ def main():
     ap.add_argument("--spmv-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-inner", type=int, default=20)
-    ap.add_argument("--orth", default="mgs", choices=["mgs", "dcgs2"],
-                    help="orthogonalisation: mgs (SciPy's sequence) or dcgs2 (one reduction per step)")
+    ap.add_argument("--orth", default="auto", choices=["auto", "mgs", "dcgs2"],
+                    help="orthogonalisation: auto (library default: dcgs2 for restart <= 32), "
+                         "mgs (SciPy's sequence) or dcgs2 (one reduction per step)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     args = ap.parse_args()
@@ -125,7 +126,7 @@ def main():
             vkcomm.init_rccl(ctx, rank, world)
         else:
             vkcomm.init_host(ctx, rank, world)
-    ctx.set_orth(vk._abi.ORTH_DCGS2 if args.orth == "dcgs2" else vk._abi.ORTH_MGS)
+    ctx.set_orth(vk._abi.ORTH[args.orth])
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
 

@@ -56,9 +56,9 @@ typedef enum { VTK_PTR_HOST = 0, VTK_PTR_DEVICE = 1 } vtk_ptr_kind;
 typedef enum {
     VTK_ORTH_MGS = 0,   /* modified Gram-Schmidt, SciPy's sequence (iterative.py:755-759):
                            j+2 dependent reductions per Arnoldi step (default)              */
-    VTK_ORTH_DCGS2 = 1  /* delayed classical GS with re-orthogonalisation: ONE reduction and
-                           two passes over the basis per step; restart <= 32; the stop test of
-                           column j runs one step later (one extra SpMV per cycle)          */
+    VTK_ORTH_DCGS2 = 1, /* delayed classical GS with re-orthogonalisation: ONE reduction and
+                           two passes over the basis per step; restart <= 32                */
+    VTK_ORTH_AUTO = 2   /* default: DCGS2 when restart <= 32, else MGS (stats.orth reports) */
 } vtk_orth;
 
 /* Synthetic Vlasov operator parameters. */

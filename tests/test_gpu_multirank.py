@@ -23,7 +23,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, case, outdir, from_host):
+def _worker(rank, world, port, case, outdir, from_host, orth):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -46,7 +46,7 @@ def _worker(rank, world, port, case, outdir, from_host):
     M = vk.block_jacobi(A, 8)
     inv = M.inverse()
     b = twin.rhs(p.n)
-    xs, info = vk.gmres(A, b[rb:re_], rtol=1e-8, M=M)
+    xs, info = vk.gmres(A, b[rb:re_], rtol=1e-8, M=M, orth=orth)
     st = vk.last_stats()
     gip, gix, gd = A.download()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), y=y, inv=inv, x=xs, info=info,
@@ -56,13 +56,14 @@ def _worker(rank, world, port, case, outdir, from_host):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,world,from_host", [("S2", 2, False), ("S4", 3, False),
-                                                  ("S2", 3, True), ("C1", 2, False)])
-def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host):
+@pytest.mark.parametrize("case,world,from_host,orth", [("S2", 2, False, "mgs"), ("S4", 3, False, "dcgs2"),
+                                                       ("S2", 3, True, "dcgs2"), ("C1", 2, False, "mgs"),
+                                                       ("C1", 2, False, "dcgs2")])
+def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 
     from oracle import coracle, twin
-    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), from_host), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), from_host, orth), nprocs=world, join=True)
     p = twin.CONFIGS[case]
     ip, ix, d = coracle.generate(p)
     inv_ref = coracle.bj_setup(ip, ix, d, 8)

@@ -169,7 +169,7 @@ def orth(request, gpu, vk_lib):
     against SciPy's MGS (same info, inner iterations +-1, x within tolerance)."""
     gpu.set_orth({"mgs": vk_lib._abi.ORTH_MGS, "dcgs2": vk_lib._abi.ORTH_DCGS2}[request.param])
     yield request.param
-    gpu.set_orth(vk_lib._abi.ORTH_MGS)
+    gpu.set_orth(vk_lib._abi.ORTH_AUTO)
 
 
 def _check_solve(xg, info, st, ref_x, ref_info, ref_iters, tol=1e-9):
@@ -252,6 +252,22 @@ def test_gmres_c1_vs_scipy_summary(ops, golden_large, orth):
     np.testing.assert_allclose(xg[:8], g["x_first8"], rtol=1e-8)
     res = np.linalg.norm(b - coracle.spmv(ip, ix, d, xg))
     assert res <= 1e-8 * g["b_norm2"]
+
+
+def test_orth_auto_default(ops):
+    import vtkrylov as vk
+    p, A, _ = ops["S2"]
+    M = vk.block_jacobi(A, 8)
+    b = twin.rhs(p.n)
+    vk.gmres(A, b, rtol=1e-8, M=M)
+    assert vk.last_stats().orth == 1                     # restart 20 -> DCGS2
+    vk.gmres(A, b, rtol=1e-8, M=M, restart=40)
+    assert vk.last_stats().orth == 0                     # restart 40 -> MGS
+    x1, _ = vk.gmres(A, b, rtol=1e-8, M=M, orth="mgs")
+    assert vk.last_stats().orth == 0
+    x2, _ = vk.gmres(A, b, rtol=1e-8, M=M)
+    assert vk.last_stats().orth == 1                     # per-call choice does not stick
+    assert np.linalg.norm(x1 - x2) / np.linalg.norm(x1) < 1e-10
 
 
 def test_gmres_device_tensors(ops, orth):

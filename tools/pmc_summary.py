@@ -24,6 +24,10 @@ CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output
     "spmv_bj": "void vtk::k_spmv<double, false, 2, 8>",
     "spmv": "void vtk::k_spmv<double, false, 0, 1>",
     "spmv_resid": "void vtk::k_spmv<double, false, 1, 1>",
+    "spmv_resid_bj": "void vtk::k_spmv<double, false, 3, 8>",
+    "dc_dots": "vtk::k_dc_dots(",
+    "dc_update": "vtk::k_dc_update(",
+    "dc_scalar": "vtk::k_dc_scalar(",
     "mgs": "vtk::k_mgs(",
     "tail": "vtk::k_tail(",
     "xupdate": "vtk::k_xupdate(",

@@ -376,35 +376,39 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const int m = s.m;
     const int64_t n = s.n;
     const double n8 = 8.0 * n;
-    auto reduce_step = [&](int j, const double *w, int col) -> int {
-        { Prof pf(c, "dc_dots", col, n8 * (j + (w ? 2 : 1)));
-          HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, col, c->stream)); }
-        { Prof pf(c, "dc_finalize", col, 0.0);
-          HIPCHK(c, launch_dc_finalize(s.dcpart, s.G, j, w != nullptr, c->d_scal, stop, col, c->stream)); }
+    // every kernel of step j is tagged j: it returns at entry once stop_col < j
+    auto reduce_step = [&](int j, const double *w, int tag) -> int {
+        { Prof pf(c, "dc_dots", tag, n8 * (j + (w ? 2 : 1)));
+          HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, tag, c->stream)); }
+        const double *part = s.dcpart;
         if (c->world > 1) {
-            Prof pf(c, "allreduce", col, 8.0 * DC_NQ);
+            { Prof pf(c, "dc_finalize", tag, 0.0);
+              HIPCHK(c, launch_dc_finalize(s.dcpart, s.G, j, w != nullptr, c->d_scal, stop, tag, c->stream)); }
+            Prof pf(c, "allreduce", tag, 8.0 * DC_NQ);
             TRY(comm_allreduce(c, c->d_scal, DC_NQ));
+            part = nullptr;
         }
-        Prof pf(c, "dc_scalar", col, 0.0);
-        HIPCHK(c, launch_dc_scalar(c->d_scal, j, m, w == nullptr, s.Hraw, s.H, s.S, s.giv, s.cf, ds, c->d_stop, c->stream));
+        Prof pf(c, "dc_scalar", tag, 0.0);
+        HIPCHK(c, launch_dc_scalar(part, s.G, c->d_scal, j, m, w == nullptr, s.Hraw, s.H, s.S, s.giv, s.cf, ds,
+                                   c->d_stop, c->stream));
         return VTK_OK;
     };
     bool broke = false;
     for (int j = 0; j < m; ++j) {
         Red h0, d0;
         double *pj = s.V + (size_t)j * s.ld;
-        TRY(precond_matvec(s, pj, s.w, stop, j - 1, h0, d0, false));
-        TRY(reduce_step(j, s.w, j - 1));
+        TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
+        TRY(reduce_step(j, s.w, j));
         { Prof pf(c, "dc_update", j, n8 * (j + 4));
           HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, c->stream)); }
         HIPCHK(c, hipEventRecord(ev[j % (LOOKAHEAD + 1)], c->stream));
         if (j >= LOOKAHEAD) {
             HIPCHK(c, hipEventSynchronize(ev[(j - LOOKAHEAD) % (LOOKAHEAD + 1)]));
-            // a stop of column cc is decided in step cc+1: act only when every rank has run it
+            // column cc stops in step cc (early commit) or cc+1: act only once every rank ran it
             if (*mirror <= j - LOOKAHEAD - 1) { broke = true; break; }
         }
     }
-    if (!broke) TRY(reduce_step(m, nullptr, m - 1));   // closing: finalise column m-1
+    if (!broke) TRY(reduce_step(m, nullptr, m));   // closing: only if column m-1 is still open
     return VTK_OK;
 }
 
@@ -422,8 +426,8 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     Solver s{A, M, c, n, round_up(std::max<int64_t>(n, 1), 64), m, grid_for(c, vector_grid(n)), nullptr, nullptr,
              nullptr, nullptr, nullptr, nullptr, nullptr, {c->d_part, c->d_part + GMAX, c->d_part + 2 * GMAX, c->d_part + 3 * GMAX}};
     // workspace: V[(m+1) x ld] | w | tmp | r | H[m x (m+1)] | S[m+1] | giv[2m]  (doubles)
-    const bool dc = c->orth == VTK_ORTH_DCGS2;
-    if (dc && m > DC_MAXJ) return fail(c, VTK_ERR_ARG, "DCGS2 supports restart <= 32");
+    const bool dc = c->orth == VTK_ORTH_DCGS2 || (c->orth == VTK_ORTH_AUTO && m <= DC_MAXJ);
+    if (dc && m > DC_MAXJ) return fail(c, VTK_ERR_ARG, "DCGS2 supports restart <= 32 (use VTK_ORTH_MGS)");
     const size_t ndc = dc ? (size_t)(m + 1) * (m + 1) + sizeof(DcCoef) / 8 + 8 + (size_t)DC_NQ * GMAX : 0;
     const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc;
     if (c->ws_bytes < nd * sizeof(double)) {
@@ -471,13 +475,36 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     Red rmb = reduce(c, s.part[1], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rmb, &ds->scal[1], 1, c->stream));
-    // r = b - A x (iterative.py:737)
-    TRY(halo_exchange(A, x));
-    { Prof pf(c, "spmv_resid", -1, b_spmv + n8);
-      HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream)); }
-    Red rr = reduce(c, s.part[2], A->tiles.grid, rc);
-    TRY(rc);
-    HIPCHK(c, launch_finalize(rr, &ds->rnorm, 1, c->stream));
+    // r = b - A x (iterative.py:737, :816).  When the BJ tiles allow (or M is the identity) the
+    // residual kernel also applies M^-1 and writes v0's direction straight into V[0]: the next
+    // cycle's psolve(r) (:742) is then already done.
+    const bool fres = !M || M->fused;
+    const Tiles *rtiles = (M && M->fused) ? &M->tiles : &A->tiles;
+    double *prr = c->d_part + 4 * GMAX, *prz = c->d_part + 5 * GMAX;
+    const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1);
+    Red rz{prz, rtiles->grid};
+    auto residual = [&]() -> int {
+        TRY(halo_exchange(A, x));
+        int rc2;
+        Red rr;
+        if (fres) {
+            Prof pf(c, "spmv_resid_bj", -1, b_csr + (M ? 8.0 * M->bs * n : 0.0) + 3 * n8);
+            HIPCHK(c, launch_spmv(spmv_in(A, rtiles, x), EPI_RESID_PREC, s.V, b, M ? M->d_inv : nullptr, M ? M->bs : 0,
+                                  nullptr, prr, prz, nullptr, 0, c->stream));
+            rr = reduce(c, prr, rtiles->grid, rc2);
+            TRY(rc2);
+            rz = reduce(c, prz, rtiles->grid, rc2);
+            TRY(rc2);
+        } else {
+            Prof pf(c, "spmv_resid", -1, b_spmv + n8);
+            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, prr, nullptr, nullptr, 0, c->stream));
+            rr = reduce(c, prr, A->tiles.grid, rc2);
+            TRY(rc2);
+        }
+        HIPCHK(c, launch_finalize(rr, &ds->rnorm, 1, c->stream));
+        return VTK_OK;
+    };
+    TRY(residual());
     HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const double bnrm2 = hs->scal[0], Mb_nrm2 = hs->scal[1];
@@ -486,7 +513,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     vtk_stats st{};
     st.bnorm = bnrm2;
     st.atol_eff = atol;
-    st.orth = c->orth;
+    st.orth = dc ? VTK_ORTH_DCGS2 : VTK_ORTH_MGS;
     auto done = [&](int inf) {
         *info = inf;
         st.t_solve = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -515,16 +542,20 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         // cycle start: v0 = M^-1 r / ||M^-1 r||, S = [tmp, 0, ...] (:742-748)
         hs->ptol = ptol;
         HIPCHK(c, hipMemcpyAsync(&ds->ptol, &hs->ptol, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        { Prof pf(c, "bj_apply", -1, b_pc);
-          HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
-        Red rv = reduce(c, s.part[0], s.G, rc);
-        TRY(rc);
+        Red rv = rz;
+        if (!fres) {
+            { Prof pf(c, "bj_apply", -1, b_pc);
+              HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
+            rv = reduce(c, s.part[0], s.G, rc);
+            TRY(rc);
+        }
         { Prof pf(c, "scale0", -1, 2 * n8);
           HIPCHK(c, launch_scale0(rv, s.V, n, s.S, m, ds, s.G, c->stream)); }
         const int *stop = &ds->stop_col;
         *mirror = BIG_COL;
         int enq = 0;
         if (dc) {
+            HIPCHK(c, hipMemsetAsync(s.cf->committed, 0, sizeof(s.cf->committed), c->stream));
             TRY(dcgs2_cycle(s, stop, mirror, ev));
         } else
         for (int col = 0; col < m; ++col) {
@@ -558,12 +589,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         const size_t xup_idx = c->prof_pending.size();
         { Prof pf(c, "xupdate", -1, 0.0);   // bytes set once the stop column is known
           HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream)); }
-        TRY(halo_exchange(A, x));
-        { Prof pf(c, "spmv_resid", -1, b_spmv + n8);
-          HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, s.part[2], nullptr, nullptr, 0, c->stream)); }
-        Red rr2 = reduce(c, s.part[2], A->tiles.grid, rc);
-        TRY(rc);
-        HIPCHK(c, launch_finalize(rr2, &ds->rnorm, 1, c->stream));
+        TRY(residual());
         HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         const int last = hs->stop_col < m ? hs->stop_col : m - 1;
@@ -930,7 +956,8 @@ void vtk_prec_destroy(vtk_prec *M) {
 }
 
 int vtk_gmres_set_orth(vtk_ctx *c, int orth) {
-    if (!c || (orth != VTK_ORTH_MGS && orth != VTK_ORTH_DCGS2)) return fail(c, VTK_ERR_ARG, "vtk_gmres_set_orth: unknown scheme");
+    if (!c || (orth != VTK_ORTH_MGS && orth != VTK_ORTH_DCGS2 && orth != VTK_ORTH_AUTO))
+        return fail(c, VTK_ERR_ARG, "vtk_gmres_set_orth: unknown scheme");
     c->orth = orth;
     return VTK_OK;
 }

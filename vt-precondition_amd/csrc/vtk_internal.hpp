@@ -42,6 +42,7 @@ struct DcCoef {
     double q;                 // 1 / (r_j * nu_{j+1})
     double nu;                // tentative h_{j+1,j}
     double h0[DC_MAXJ + 1];   // ||B v_c|| per column (breakdown test, iterative.py:766)
+    int committed[DC_MAXJ + 1];   // column already rotated into H (early or exact commit)
 };
 
 // a reduced scalar as seen by a consumer kernel: G partials (single GPU) or 1 value (after
@@ -71,7 +72,7 @@ struct vtk_ctx {
     ncclComm_t comm = nullptr;            // RCCL (production transport)
     bool host_comm = false;               // host-staged hooks (vtk_comm_init_host)
     vtk_host_comm hops{};
-    int orth = VTK_ORTH_MGS;
+    int orth = VTK_ORTH_AUTO;
     // scratch shared by calls on this context
     double *d_part = nullptr;        // [8][GMAX] partial sums
     double *d_scal = nullptr;        // [256] reduced scalars (all-reduce slots)
@@ -131,10 +132,11 @@ struct SpmvIn {
     const double *x, *halo;   // halo may be null (world == 1)
 };
 
-enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2 };
+enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2, EPI_RESID_PREC = 3 };
 
 // y = A x (PLAIN); y = b - A x, part0 = sum y^2 (RESID); y = M^-1 A x with M = BJ(inv, bs)
-// or identity (inv == null), part0 = sum y^2, part1 = sum v0*y (PREC, v0 may be null).
+// or identity (inv == null), part0 = sum y^2, part1 = sum v0*y (PREC, v0 may be null);
+// RESID_PREC: r = b - A x, y = M^-1 r, part0 = sum r^2, part1 = sum y^2.
 hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
                        int bs, const double *v0, double *part0, double *part1,
                        const int *stop_col, int col, hipStream_t s);
@@ -185,9 +187,10 @@ hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, i
                           double *part, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, double *scal,
                               const int *stop_col, int col, hipStream_t s);
-hipError_t launch_dc_scalar(const double *scal, int j, int m, int closing, double *Hraw,
-                            double *H, double *S, double *giv, DcCoef *cf, GmresState *st,
-                            int *stop_map, hipStream_t s);
+// part != null: reduce the G partials in-kernel (one GPU); else read the all-reduced scal
+hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int j, int m,
+                            int closing, double *Hraw, double *H, double *S, double *giv,
+                            DcCoef *cf, GmresState *st, int *stop_map, hipStream_t s);
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
                             const DcCoef *cf, int grid, const int *stop_col, hipStream_t s);
 

@@ -156,7 +156,13 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
                         acc0 += r * r;
                     }
                 } else {
-                    double z = s;
+                    // PREC: z = M^-1 (A x);  RESID_PREC: r = b - A x (iterative.py:816), z = M^-1 r
+                    double sv = s;
+                    if constexpr (EPI == EPI_RESID_PREC) {
+                        sv = act ? a.b[row] - s : 0.0;
+                        acc0 += sv * sv;
+                    }
+                    double z = sv;
                     if constexpr (BS > 0) {
                         // z_i = sum_j inv[i][j] * y_j over the BS lanes of this block
                         double m[BS];
@@ -165,14 +171,18 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
                         z = 0.0;
 #pragma unroll
                         for (int j = 0; j < BS; ++j) {
-                            const double yj = __shfl(s, gb + j, 64);
+                            const double yj = __shfl(sv, gb + j, 64);
                             if (act) z += m[j] * yj;
                         }
                     }
                     if (act) {
                         a.y[row] = z;
-                        acc0 += z * z;
-                        if (a.v0) acc1 += a.v0[row] * z;
+                        if constexpr (EPI == EPI_RESID_PREC) {
+                            acc1 += z * z;
+                        } else {
+                            acc0 += z * z;
+                            if (a.v0) acc1 += a.v0[row] * z;
+                        }
                     }
                 }
             }
@@ -192,6 +202,11 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
                         const double r = a.b[row] - s;
                         a.y[row] = r;
                         acc0 += r * r;
+                    } else if constexpr (EPI == EPI_RESID_PREC) {
+                        const double r = a.b[row] - s;   // BS == 0 only (host guarantees)
+                        a.y[row] = r;
+                        acc0 += r * r;
+                        acc1 += r * r;
                     } else {
                         a.y[row] = s;   // BS == 0 only (host guarantees)
                         acc0 += s * s;
@@ -204,7 +219,7 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
     if constexpr (EPI != EPI_PLAIN) {
         const double t0 = block_sum(acc0, red);
         if (tid == 0) a.part0[blockIdx.x] = t0;
-        if (EPI == EPI_PREC && a.v0 != nullptr) {
+        if (EPI == EPI_RESID_PREC || (EPI == EPI_PREC && a.v0 != nullptr)) {
             const double t1 = block_sum(acc1, red);
             if (tid == 0) a.part1[blockIdx.x] = t1;
         }
@@ -223,7 +238,7 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
         hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1>), g, blk, 0, s, a);
     } else if (epi == EPI_RESID) {
         hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID, 1>), g, blk, 0, s, a);
-    } else {
+    } else if (epi == EPI_PREC) {
         if (inv == nullptr) bs = 0;
         switch (bs) {
             case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 0>), g, blk, 0, s, a); break;
@@ -233,6 +248,18 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
             case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 8>), g, blk, 0, s, a); break;
             case 16: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 16>), g, blk, 0, s, a); break;
             case 32: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 32>), g, blk, 0, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        if (inv == nullptr) bs = 0;
+        switch (bs) {
+            case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 0>), g, blk, 0, s, a); break;
+            case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 1>), g, blk, 0, s, a); break;
+            case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 2>), g, blk, 0, s, a); break;
+            case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 4>), g, blk, 0, s, a); break;
+            case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 8>), g, blk, 0, s, a); break;
+            case 16: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 16>), g, blk, 0, s, a); break;
+            case 32: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 32>), g, blk, 0, s, a); break;
             default: return hipErrorInvalidValue;
         }
     }
@@ -895,37 +922,64 @@ hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, do
     return hipGetLastError();
 }
 
-// single lane: re-orthogonalisation scalars, column j-1 finalisation + SciPy's Givens/stop
-// logic (iterative.py:761-794), tentative column j and the update-pass coefficients
-__global__ void k_dc_scalar(const double *scal, int j, int m, int closing, double *Hraw, double *H,
-                            double *S, double *giv, DcCoef *cf, GmresState *st, int *stop_map) {
-    if (threadIdx.x != 0 || st->stop_col < j - 1) return;
-    const double *sv = scal, *zv = scal + DC_MAXJ;
-    const double alpha = scal[2 * DC_MAXJ], beta = scal[2 * DC_MAXJ + 1], gamma = scal[2 * DC_MAXJ + 2];
+// Scalar step of DCGS2 step j (one workgroup; lane 0 does the O(j^2) algebra from LDS):
+//  * quantities: reduced here from the G partials (one GPU) or read from scal (all-reduced);
+//  * j >= 1: re-orthogonalisation scalars of p_j, finalise column j-1 (h += nu s,
+//    h_{j,j-1} = nu r) unless it was already committed, SciPy's Givens/stop logic on it
+//    (iterative.py:761-794);
+//  * closing == 0: tentative column j and the update-pass coefficients; the column is committed
+//    at once (Givens, stop test) when its estimate is numerically safe — no cancellation in
+//    nu (nu > 1e-3 ||Bv||) and presid not within 1e-8 of ptol — or it is the cycle's last
+//    column; otherwise it is finalised exactly by step j+1.
+__global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt, const double *scal, int j,
+                                                    int m, int closing, double *Hraw, double *H,
+                                                    double *S, double *giv, DcCoef *cf,
+                                                    GmresState *st, int *stop_map) {
+    __shared__ double q[DC_NQ];
+    __shared__ double hr_s[(DC_MAXJ + 1) * (DC_MAXJ + 1)];
+    __shared__ double giv_s[2 * DC_MAXJ];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+    if (st->stop_col < j) return;
+    const int with_w = closing ? 0 : 1;
+    const int nq = with_w ? 2 * j + 3 : j + 1;
+    for (int b = wv; b < nq; b += nw) {      // quantity b -> slot
+        int qs;
+        if (b < j) qs = b;
+        else if (with_w && b < 2 * j) qs = DC_MAXJ + (b - j);
+        else qs = 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
+        double acc = 0.0;
+        if (part) {
+            for (int i = lane; i < cnt; i += 64) acc += part[(size_t)qs * GMAX + i];
+            acc = wave_sum(acc);
+        } else {
+            acc = scal[qs];
+        }
+        if (lane == 0) q[qs] = acc;
+    }
     const int M1 = m + 1;
+    for (int e = tid; e < j * (j + 1); e += blockDim.x) {   // raw columns 0..j-1, rows 0..j
+        const int i = e / (j + 1), k = e % (j + 1);
+        hr_s[i * (DC_MAXJ + 1) + k] = Hraw[(size_t)i * M1 + k];
+    }
+    for (int e = tid; e < 2 * j; e += blockDim.x) giv_s[e] = giv[e];
+    __syncthreads();
+    if (tid != 0) return;
+    const double *sv = q, *zv = q + DC_MAXJ;
+    const double alpha = q[2 * DC_MAXJ], beta = q[2 * DC_MAXJ + 1], gamma = q[2 * DC_MAXJ + 2];
+    const double ptol = st->ptol;
     double r = 1.0;
-    if (j >= 1) {
-        double ss = 0.0;
-        for (int k = 0; k < j; ++k) ss += sv[k] * sv[k];
-        const double r2 = alpha - ss;
-        r = __builtin_sqrt(r2 > 0.0 ? r2 : alpha);
-        const int c = j - 1;
-        double *hr = Hraw + (size_t)c * M1;
-        const double nu = cf->nu;
-        for (int k = 0; k < j; ++k) hr[k] = hr[k] + nu * sv[k];
-        hr[j] = nu * r;
-        double *hc = H + (size_t)c * M1;
-        for (int k = 0; k <= j; ++k) hc[k] = hr[k];
-        const bool brk = hc[j] <= DBL_EPSILON * cf->h0[c];
-        if (brk) hc[j] = 0.0;
+    // Givens + stop test on column c (rows 0..c+1 in hc), SciPy's order
+    auto rotate_commit = [&](int c, double *hc, bool brk) -> bool {
         for (int k = 0; k < c; ++k) {
-            const double cg = giv[2 * k], sg = giv[2 * k + 1];
+            const double cg = giv_s[2 * k], sg = giv_s[2 * k + 1];
             const double n0 = hc[k], n1 = hc[k + 1];
             hc[k] = cg * n0 + sg * n1;
             hc[k + 1] = -sg * n0 + cg * n1;
         }
         double cg, sg, mag;
         d_lartg(hc[c], hc[c + 1], cg, sg, mag);
+        giv_s[2 * c] = cg;
+        giv_s[2 * c + 1] = sg;
         giv[2 * c] = cg;
         giv[2 * c + 1] = sg;
         hc[c] = mag;
@@ -936,14 +990,34 @@ __global__ void k_dc_scalar(const double *scal, int j, int m, int closing, doubl
         const double presid = __builtin_fabs(t);
         st->presid = presid;
         st->inner += 1;
-        if (presid <= st->ptol || brk || closing) {
-            if (presid <= st->ptol || brk) {
-                st->breakdown = brk ? 1 : 0;
-                st->stop_col = c;
-                if (stop_map) __hip_atomic_store(stop_map, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            return;
+        if (presid <= ptol || brk) {
+            st->breakdown = brk ? 1 : 0;
+            st->stop_col = c;
+            if (stop_map) __hip_atomic_store(stop_map, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return true;
         }
+        return false;
+    };
+    if (j >= 1) {
+        double ss = 0.0;
+        for (int k = 0; k < j; ++k) ss += sv[k] * sv[k];
+        const double r2 = alpha - ss;
+        r = __builtin_sqrt(r2 > 0.0 ? r2 : alpha);
+        const int c = j - 1;
+        if (!cf->committed[c]) {
+            double *hr = hr_s + c * (DC_MAXJ + 1);
+            const double nu = cf->nu;
+            for (int k = 0; k < j; ++k) hr[k] = hr[k] + nu * sv[k];
+            hr[j] = nu * r;
+            for (int k = 0; k <= j; ++k) Hraw[(size_t)c * M1 + k] = hr[k];
+            double *hc = H + (size_t)c * M1;
+            for (int k = 0; k <= j; ++k) hc[k] = hr[k];
+            const bool brk = hc[j] <= DBL_EPSILON * cf->h0[c];
+            if (brk) hc[j] = 0.0;
+            cf->committed[c] = 1;
+            if (rotate_commit(c, hc, brk)) return;
+        }
+        if (closing) return;
     }
     // tentative column j
     cf->rinv = 1.0 / r;
@@ -951,29 +1025,57 @@ __global__ void k_dc_scalar(const double *scal, int j, int m, int closing, doubl
     double sz = 0.0;
     for (int k = 0; k < j; ++k) sz += sv[k] * zv[k];
     double ee = 0.0;
-    double *hj = Hraw + (size_t)j * M1;
+    double hj[DC_MAXJ + 2];
     for (int k = 0; k <= j; ++k) {
         const double e = k < j ? zv[k] : (beta - sz) / r;
         cf->e[k] = e;
         ee += e * e;
         double g = 0.0;   // (H_j s)_k over the final raw columns i < j (row k nonzero for i >= k-1)
-        for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) g += Hraw[(size_t)i * M1 + k] * sv[i];
+        for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) g += hr_s[i * (DC_MAXJ + 1) + k] * sv[i];
         hj[k] = (e - g) / r;
+        Hraw[(size_t)j * M1 + k] = hj[k];
     }
     const double gn = __builtin_sqrt(gamma) / r;
     const double nu2 = gamma - ee;
     double nu = nu2 > 0.0 ? __builtin_sqrt(nu2) / r : 0.0;
-    if (!(nu > 1e-8 * gn)) nu = gn > 0.0 ? gn : 1.0;   // cancellation: r of the next step corrects
+    const bool safe = nu > 1e-3 * gn;
+    if (!(nu > 1e-8 * gn)) nu = gn > 0.0 ? gn : 1.0;   // heavy cancellation: step j+1's r corrects
     cf->nu = nu;
     cf->h0[j] = gn;
     cf->q = 1.0 / (r * nu);
+    cf->committed[j] = 0;
+    if (!safe) return;
+    // trial rotation of the tentative column: commit now if the decision is unambiguous
+    double t[DC_MAXJ + 2];
+    for (int k = 0; k <= j; ++k) t[k] = hj[k];
+    t[j + 1] = nu;
+    for (int k = 0; k < j; ++k) {
+        const double cg = giv_s[2 * k], sg = giv_s[2 * k + 1];
+        const double n0 = t[k], n1 = t[k + 1];
+        t[k] = cg * n0 + sg * n1;
+        t[k + 1] = -sg * n0 + cg * n1;
+    }
+    double cg, sg, mag;
+    d_lartg(t[j], t[j + 1], cg, sg, mag);
+    const double pres_t = __builtin_fabs(-sg * S[j]);
+    const bool last = j == m - 1;
+    if (!(last || pres_t <= ptol * (1.0 - 1e-8) || pres_t > ptol * (1.0 + 1e-8))) return;
+    if (!(last || pres_t <= ptol * (1.0 - 1e-8))) return;   // clearly above ptol: defer exactly
+    double *hc = H + (size_t)j * M1;
+    for (int k = 0; k <= j; ++k) hc[k] = hj[k];
+    hc[j + 1] = nu;
+    cf->committed[j] = 1;
+    if (!rotate_commit(j, hc, false) && last) {
+        st->stop_col = j;   // cycle complete: later kernels of this cycle are no-ops
+        if (stop_map) __hip_atomic_store(stop_map, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-hipError_t launch_dc_scalar(const double *scal, int j, int m, int closing, double *Hraw, double *H,
-                            double *S, double *giv, DcCoef *cf, GmresState *st, int *stop_map,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(k_dc_scalar, dim3(1), dim3(64), 0, s, scal, j, m, closing, Hraw, H, S, giv, cf, st,
-                       stop_map);
+hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int j, int m, int closing,
+                            double *Hraw, double *H, double *S, double *giv, DcCoef *cf, GmresState *st,
+                            int *stop_map, hipStream_t s) {
+    hipLaunchKernelGGL(k_dc_scalar, dim3(1), dim3(1024), 0, s, part, cnt, scal, j, m, closing, Hraw, H, S, giv,
+                       cf, st, stop_map);
     return hipGetLastError();
 }
 

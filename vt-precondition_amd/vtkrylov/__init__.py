@@ -131,8 +131,11 @@ class Context:
                                         "gbs": e.bytes / e.seconds / 1e9 if e.seconds > 0 else 0.0}
         return out
 
+    orth = _abi.ORTH_AUTO
+
     def set_orth(self, orth: int):
         check(lib().vtk_gmres_set_orth(self._h, int(orth)), self._h)
+        self.orth = int(orth)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -329,13 +332,15 @@ def last_stats() -> SolveStats | None:
 
 
 def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=None,
-          callback=None, callback_type=None):
+          callback=None, callback_type=None, orth=None):
     """``scipy.sparse.linalg.gmres`` on the GPU (iterative.py:582-841, left-preconditioned
     restarted GMRES with modified Gram-Schmidt).  Returns ``(x, info)``.
 
     ``A``: a :class:`CsrOperator` or any SciPy sparse matrix (uploaded).  ``M``: None or a
     :class:`BlockJacobi` built on ``A``; any other preconditioner raises TypeError (no CPU
     fallback).  ``callback`` is not supported (the Arnoldi loop never returns to the host).
+    ``orth`` (extension): "mgs" (SciPy's exact sequence), "dcgs2" (one reduction per step,
+    restart <= 32) or "auto"/None (the context's setting; default DCGS2 when restart <= 32).
     """
     global _last_stats
     if callback is not None:
@@ -365,10 +370,18 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     x = vx.obj
     info = C.c_int()
     st = _abi.Stats()
-    check(lib().vtk_gmres(A.handle, None if M is None else M.handle, vb.ptr, vx.ptr,
-                          float(rtol), float(atol), 0 if restart is None else int(restart),
-                          0 if maxiter is None else int(maxiter), vb.kind, C.byref(info),
-                          C.byref(st)), A.ctx.handle)
+    prev = None
+    if orth is not None:
+        prev = A.ctx.orth
+        A.ctx.set_orth(_abi.ORTH[orth])
+    try:
+        check(lib().vtk_gmres(A.handle, None if M is None else M.handle, vb.ptr, vx.ptr,
+                              float(rtol), float(atol), 0 if restart is None else int(restart),
+                              0 if maxiter is None else int(maxiter), vb.kind, C.byref(info),
+                              C.byref(st)), A.ctx.handle)
+    finally:
+        if prev is not None:
+            A.ctx.set_orth(prev)
     _last_stats = SolveStats(**st.as_dict())
     return x, info.value
 

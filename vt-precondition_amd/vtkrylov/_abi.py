@@ -27,6 +27,8 @@ PTR_DEVICE = 1
 
 ORTH_MGS = 0
 ORTH_DCGS2 = 1
+ORTH_AUTO = 2
+ORTH = {"mgs": 0, "dcgs2": 1, "auto": 2}
 
 
 class VlasovParams(C.Structure):
