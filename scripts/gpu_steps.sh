@@ -24,10 +24,15 @@ for s in "$@"; do
         testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         bench) step bench 600 python bench.py ;;
         benchq) step benchq 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        benchc4) step benchc4 600 python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 ;;
+        benchc2) step benchc2 300 python bench.py --config C2 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        benchc1) step benchc1 300 python bench.py --config C1 --steps 5 --warmup 1 --no-cpu-baseline ;;
+        benchmgs) step benchmgs 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth mgs ;;
         benchdc) step benchdc 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth dcgs2 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         multirank) step multirank 900 python -m pytest tests/test_gpu_multirank.py -m gpu -x -q -p no:cacheprovider ;;
         bench2host) step bench2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --comm host --config C1 --steps 1 --warmup 1 --spmv-reps 3 ;;
+        profc1) step profc1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc1 -o run --output-format csv -- python bench.py --config C1 --steps 3 --warmup 1 --no-cpu-baseline ;;
         pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
         pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
         *) echo "unknown step $s"; exit 2 ;;

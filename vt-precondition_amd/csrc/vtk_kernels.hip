@@ -41,10 +41,25 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
     return s;
 }
 
+// sum of p[i0], p[i0+STRIDE], ... (< cnt <= U*STRIDE) in that order, with every load issued
+// before the first add (a rolled loop paid one L2 round trip per element)
+template <int U, int STRIDE>
+__device__ __forceinline__ double strided_sum(const double *p, int cnt, int i0) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * STRIDE;
+        v[u] = i < cnt ? p[i] : 0.0;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+    return acc;
+}
+static_assert(GMAX <= 4 * NT && GMAX <= 16 * 64, "partial-sum unroll bounds");
+
 __device__ __forceinline__ double reduce_red(Red r, double *red) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < r.cnt; i += NT) s += r.p[i];
-    return block_sum(s, red);
+    return block_sum(strided_sum<GMAX / NT, NT>(r.p, r.cnt, threadIdx.x), red);
 }
 
 __device__ __forceinline__ bool stopped(const int *stop_col, int col) {
@@ -585,8 +600,13 @@ __global__ __launch_bounds__(NT) void k_tail(Red h0r, Red w2r, const double *__r
             vn[i] = w[i] * sc;
         }
     }
+    __shared__ double hcs[MAX_RESTART + 1];
+    if (blockIdx.x == 0) {   // LDS copy of column col: the rotation chain never touches global memory
+        for (int k = threadIdx.x; k <= col; k += NT) hcs[k] = H[(size_t)col * (m + 1) + k];
+        __syncthreads();
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        double *hc = H + (size_t)col * (m + 1);
+        double *hc = hcs;
         hc[col + 1] = brk ? 0.0 : h1;
         for (int k = 0; k < col; ++k) {
             const double c = giv[2 * k], s = giv[2 * k + 1];
@@ -600,6 +620,8 @@ __global__ __launch_bounds__(NT) void k_tail(Red h0r, Red w2r, const double *__r
         giv[2 * col + 1] = s;
         hc[col] = mag;
         hc[col + 1] = 0.0;
+        double *hg = H + (size_t)col * (m + 1);
+        for (int k = 0; k <= col + 1; ++k) hg[k] = hc[k];
         const double t = -s * S[col];
         S[col] = c * S[col];
         S[col + 1] = t;
@@ -909,9 +931,7 @@ __global__ __launch_bounds__(NT) void k_dc_finalize(const double *part, int cnt,
     if (b < j) q = b;
     else if (with_w && b < 2 * j) q = DC_MAXJ + (b - j);
     else q = 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < cnt; i += NT) acc += part[(size_t)q * GMAX + i];
-    const double t = block_sum(acc, red);
+    const double t = block_sum(strided_sum<GMAX / NT, NT>(part + (size_t)q * GMAX, cnt, threadIdx.x), red);
     if (threadIdx.x == 0) scal[q] = t;
 }
 
@@ -938,38 +958,45 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
     __shared__ double q[DC_NQ];
     __shared__ double hr_s[(DC_MAXJ + 1) * (DC_MAXJ + 1)];
     __shared__ double giv_s[2 * DC_MAXJ];
+    __shared__ double S_s[DC_MAXJ + 2], hc_s[DC_MAXJ + 2], hj[DC_MAXJ + 2], e_s[DC_MAXJ + 2];
+    __shared__ double sc[8];   // ptol, nu(prev), h0(prev), r, sz
+    __shared__ int flags[2];   // committed(prev), done
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     if (st->stop_col < j) return;
     const int with_w = closing ? 0 : 1;
     const int nq = with_w ? 2 * j + 3 : j + 1;
-    for (int b = wv; b < nq; b += nw) {      // quantity b -> slot
+    const int M1 = m + 1;
+    // phase A: quantities, raw Hessenberg columns 0..j-1, rotations, S, scalars -> LDS
+    for (int b = wv; b < nq; b += nw) {
         int qs;
         if (b < j) qs = b;
         else if (with_w && b < 2 * j) qs = DC_MAXJ + (b - j);
         else qs = 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
-        double acc = 0.0;
-        if (part) {
-            for (int i = lane; i < cnt; i += 64) acc += part[(size_t)qs * GMAX + i];
-            acc = wave_sum(acc);
-        } else {
-            acc = scal[qs];
-        }
+        const double acc = part ? wave_sum(strided_sum<GMAX / 64, 64>(part + (size_t)qs * GMAX, cnt, lane))
+                                : scal[qs];
         if (lane == 0) q[qs] = acc;
     }
-    const int M1 = m + 1;
-    for (int e = tid; e < j * (j + 1); e += blockDim.x) {   // raw columns 0..j-1, rows 0..j
+    for (int e = tid; e < j * (j + 1); e += blockDim.x) {
         const int i = e / (j + 1), k = e % (j + 1);
         hr_s[i * (DC_MAXJ + 1) + k] = Hraw[(size_t)i * M1 + k];
     }
     for (int e = tid; e < 2 * j; e += blockDim.x) giv_s[e] = giv[e];
+    for (int e = tid; e <= m && e < DC_MAXJ + 2; e += blockDim.x) S_s[e] = S[e];
+    if (tid == 0) {
+        sc[0] = st->ptol;
+        sc[1] = j >= 1 ? cf->nu : 0.0;
+        sc[2] = j >= 1 ? cf->h0[j - 1] : 0.0;
+        flags[0] = j >= 1 ? cf->committed[j - 1] : 1;
+        flags[1] = 0;
+    }
     __syncthreads();
-    if (tid != 0) return;
     const double *sv = q, *zv = q + DC_MAXJ;
     const double alpha = q[2 * DC_MAXJ], beta = q[2 * DC_MAXJ + 1], gamma = q[2 * DC_MAXJ + 2];
-    const double ptol = st->ptol;
-    double r = 1.0;
-    // Givens + stop test on column c (rows 0..c+1 in hc), SciPy's order
-    auto rotate_commit = [&](int c, double *hc, bool brk) -> bool {
+    const double ptol = sc[0];
+    // Givens + stop test on the LDS column hc_s (rows 0..c+1), SciPy's order; the rotated
+    // column, S and the rotation go to global memory once
+    auto rotate_commit = [&](int c, bool brk) -> bool {
+        double *hc = hc_s;
         for (int k = 0; k < c; ++k) {
             const double cg = giv_s[2 * k], sg = giv_s[2 * k + 1];
             const double n0 = hc[k], n1 = hc[k + 1];
@@ -984,8 +1011,12 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
         giv[2 * c + 1] = sg;
         hc[c] = mag;
         hc[c + 1] = 0.0;
-        const double t = -sg * S[c];
-        S[c] = cg * S[c];
+        double *hg = H + (size_t)c * M1;
+        for (int k = 0; k <= c + 1; ++k) hg[k] = hc[k];
+        const double t = -sg * S_s[c];
+        S_s[c] = cg * S_s[c];
+        S_s[c + 1] = t;
+        S[c] = S_s[c];
         S[c + 1] = t;
         const double presid = __builtin_fabs(t);
         st->presid = presid;
@@ -998,43 +1029,54 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
         }
         return false;
     };
-    if (j >= 1) {
-        double ss = 0.0;
-        for (int k = 0; k < j; ++k) ss += sv[k] * sv[k];
-        const double r2 = alpha - ss;
-        r = __builtin_sqrt(r2 > 0.0 ? r2 : alpha);
-        const int c = j - 1;
-        if (!cf->committed[c]) {
+    // phase B (lane 0): r, finalise column j-1 (h += nu s, h_{j,j-1} = nu r) and rotate it
+    if (tid == 0) {
+        double ss = 0.0, sz = 0.0;
+        for (int k = 0; k < j; ++k) { ss += sv[k] * sv[k]; sz += sv[k] * zv[k]; }
+        double r = 1.0;
+        if (j >= 1) {
+            const double r2 = alpha - ss;
+            r = __builtin_sqrt(r2 > 0.0 ? r2 : alpha);
+        }
+        sc[3] = r;
+        sc[4] = sz;
+        if (j >= 1 && !flags[0]) {
+            const int c = j - 1;
             double *hr = hr_s + c * (DC_MAXJ + 1);
-            const double nu = cf->nu;
+            const double nu = sc[1];
             for (int k = 0; k < j; ++k) hr[k] = hr[k] + nu * sv[k];
             hr[j] = nu * r;
-            for (int k = 0; k <= j; ++k) Hraw[(size_t)c * M1 + k] = hr[k];
-            double *hc = H + (size_t)c * M1;
-            for (int k = 0; k <= j; ++k) hc[k] = hr[k];
-            const bool brk = hc[j] <= DBL_EPSILON * cf->h0[c];
-            if (brk) hc[j] = 0.0;
+            for (int k = 0; k <= j; ++k) { Hraw[(size_t)c * M1 + k] = hr[k]; hc_s[k] = hr[k]; }
+            const bool brk = hc_s[j] <= DBL_EPSILON * sc[2];
+            if (brk) hc_s[j] = 0.0;
             cf->committed[c] = 1;
-            if (rotate_commit(c, hc, brk)) return;
+            if (rotate_commit(c, brk)) flags[1] = 1;
         }
-        if (closing) return;
+        if (closing) flags[1] = 1;
     }
-    // tentative column j
-    cf->rinv = 1.0 / r;
-    for (int k = 0; k < j; ++k) cf->s[k] = sv[k];
-    double sz = 0.0;
-    for (int k = 0; k < j; ++k) sz += sv[k] * zv[k];
-    double ee = 0.0;
-    double hj[DC_MAXJ + 2];
-    for (int k = 0; k <= j; ++k) {
-        const double e = k < j ? zv[k] : (beta - sz) / r;
-        cf->e[k] = e;
-        ee += e * e;
-        double g = 0.0;   // (H_j s)_k over the final raw columns i < j (row k nonzero for i >= k-1)
+    __syncthreads();
+    if (flags[1]) return;
+    // phase C (lanes k <= j): tentative column j, c'_k = (e_k - (H_j s)_k) / r, with the raw
+    // columns i < j final; row k of column i is nonzero for i >= k-1
+    const double r = sc[3];
+    if (tid <= j) {
+        const int k = tid;
+        const double e = k < j ? zv[k] : (beta - sc[4]) / r;
+        double g = 0.0;
         for (int i = (k > 0 ? k - 1 : 0); i < j; ++i) g += hr_s[i * (DC_MAXJ + 1) + k] * sv[i];
-        hj[k] = (e - g) / r;
-        Hraw[(size_t)j * M1 + k] = hj[k];
+        const double h = (e - g) / r;
+        e_s[k] = e;
+        hj[k] = h;
+        Hraw[(size_t)j * M1 + k] = h;
+        cf->e[k] = e;
+        if (k < j) cf->s[k] = sv[k];
     }
+    __syncthreads();
+    if (tid != 0) return;
+    // phase D (lane 0): nu_{j+1}, update-pass scalars, early commit when unambiguous
+    double ee = 0.0;
+    for (int k = 0; k <= j; ++k) ee += e_s[k] * e_s[k];
+    cf->rinv = 1.0 / r;
     const double gn = __builtin_sqrt(gamma) / r;
     const double nu2 = gamma - ee;
     double nu = nu2 > 0.0 ? __builtin_sqrt(nu2) / r : 0.0;
@@ -1045,27 +1087,18 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
     cf->q = 1.0 / (r * nu);
     cf->committed[j] = 0;
     if (!safe) return;
-    // trial rotation of the tentative column: commit now if the decision is unambiguous
-    double t[DC_MAXJ + 2];
-    for (int k = 0; k <= j; ++k) t[k] = hj[k];
-    t[j + 1] = nu;
-    for (int k = 0; k < j; ++k) {
-        const double cg = giv_s[2 * k], sg = giv_s[2 * k + 1];
-        const double n0 = t[k], n1 = t[k + 1];
-        t[k] = cg * n0 + sg * n1;
-        t[k + 1] = -sg * n0 + cg * n1;
-    }
+    // trial rotation of the tentative column (only the last rotated entry is needed)
+    double a0 = hj[0];
+    for (int k = 0; k < j; ++k) a0 = -giv_s[2 * k + 1] * a0 + giv_s[2 * k] * hj[k + 1];
     double cg, sg, mag;
-    d_lartg(t[j], t[j + 1], cg, sg, mag);
-    const double pres_t = __builtin_fabs(-sg * S[j]);
+    d_lartg(a0, nu, cg, sg, mag);
+    const double pres_t = __builtin_fabs(-sg * S_s[j]);
     const bool last = j == m - 1;
-    if (!(last || pres_t <= ptol * (1.0 - 1e-8) || pres_t > ptol * (1.0 + 1e-8))) return;
-    if (!(last || pres_t <= ptol * (1.0 - 1e-8))) return;   // clearly above ptol: defer exactly
-    double *hc = H + (size_t)j * M1;
-    for (int k = 0; k <= j; ++k) hc[k] = hj[k];
-    hc[j + 1] = nu;
+    if (!(last || pres_t <= ptol * (1.0 - 1e-8))) return;   // above or ambiguous: finalise exactly
+    for (int k = 0; k <= j; ++k) hc_s[k] = hj[k];
+    hc_s[j + 1] = nu;
     cf->committed[j] = 1;
-    if (!rotate_commit(j, hc, false) && last) {
+    if (!rotate_commit(j, false) && last) {
         st->stop_col = j;   // cycle complete: later kernels of this cycle are no-ops
         if (stop_map) __hip_atomic_store(stop_map, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
