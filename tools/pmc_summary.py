@@ -25,6 +25,7 @@ CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output
     "spmv": "void vtk::k_spmv<double, false, 0, 1>",
     "spmv_resid": "void vtk::k_spmv<double, false, 1, 1>",
     "spmv_resid_bj": "void vtk::k_spmv<double, false, 3, 8>",
+    "spmv_bj_dc": "void vtk::k_spmv<double, false, 4, 8>",
     "dc_dots": "vtk::k_dc_dots(",
     "dc_update": "vtk::k_dc_update(",
     "dc_scalar": "vtk::k_dc_scalar(",

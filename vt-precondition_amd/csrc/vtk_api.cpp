@@ -377,28 +377,47 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const int64_t n = s.n;
     const double n8 = 8.0 * n;
     // every kernel of step j is tagged j: it returns at entry once stop_col < j
-    auto reduce_step = [&](int j, const double *w, int tag) -> int {
-        { Prof pf(c, "dc_dots", tag, n8 * (j + (w ? 2 : 1)));
-          HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, tag, c->stream)); }
+    // SpMV + BJ and the step's dots in one pass for BJ-fused tiles with bs <= 8 (larger blocks
+    // would spill the fused kernel's registers)
+    const bool fused = s.M && s.M->fused && s.M->bs <= 8;
+    const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
+    const double b_csr = (s.A->fp32 ? 8.0 : 12.0) * s.A->nnz + 4.0 * (n + 1);
+    const double b_inv = s.M ? 8.0 * s.M->bs * n : 0.0;
+    // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
+    auto reduce_step = [&](int j, const double *w, int tag, int cnt) -> int {
+        if (cnt == 0) {
+            Prof pf(c, "dc_dots", tag, n8 * (j + (w ? 2 : 1)));
+            HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, tag, c->stream));
+            cnt = s.G;
+        }
         const double *part = s.dcpart;
         if (c->world > 1) {
             { Prof pf(c, "dc_finalize", tag, 0.0);
-              HIPCHK(c, launch_dc_finalize(s.dcpart, s.G, j, w != nullptr, c->d_scal, stop, tag, c->stream)); }
+              HIPCHK(c, launch_dc_finalize(s.dcpart, cnt, j, w != nullptr, c->d_scal, stop, tag, c->stream)); }
             Prof pf(c, "allreduce", tag, 8.0 * DC_NQ);
             TRY(comm_allreduce(c, c->d_scal, DC_NQ));
             part = nullptr;
         }
         Prof pf(c, "dc_scalar", tag, 0.0);
-        HIPCHK(c, launch_dc_scalar(part, s.G, c->d_scal, j, m, w == nullptr, s.Hraw, s.H, s.S, s.giv, s.cf, ds,
+        HIPCHK(c, launch_dc_scalar(part, cnt, c->d_scal, j, m, w == nullptr, s.Hraw, s.H, s.S, s.giv, s.cf, ds,
                                    c->d_stop, c->stream));
         return VTK_OK;
     };
     bool broke = false;
     for (int j = 0; j < m; ++j) {
-        Red h0, d0;
         double *pj = s.V + (size_t)j * s.ld;
-        TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
-        TRY(reduce_step(j, s.w, j));
+        int cnt = 0;
+        if (fused) {
+            TRY(halo_exchange(s.A, pj));
+            Prof pf(c, "spmv_bj_dc", j, b_csr + b_inv + n8 * (j + 2));   // CSR, BJ, p, w, V_j
+            HIPCHK(c, launch_spmv_dc(spmv_in(s.A, ft, pj), s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j, s.dcpart,
+                                     stop, j, c->stream));
+            cnt = ft->grid;
+        } else {
+            Red h0, d0;
+            TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
+        }
+        TRY(reduce_step(j, s.w, j, cnt));
         { Prof pf(c, "dc_update", j, n8 * (j + 4));
           HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, c->stream)); }
         HIPCHK(c, hipEventRecord(ev[j % (LOOKAHEAD + 1)], c->stream));
@@ -408,7 +427,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             if (*mirror <= j - LOOKAHEAD - 1) { broke = true; break; }
         }
     }
-    if (!broke) TRY(reduce_step(m, nullptr, m));   // closing: only if column m-1 is still open
+    if (!broke) TRY(reduce_step(m, nullptr, m, 0));   // closing: only if column m-1 is still open
     return VTK_OK;
 }
 
@@ -432,8 +451,6 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
-    prof_flush(c);
-    for (auto e : c->prof_pool) (void)hipEventDestroy(e);
         c->ws = nullptr;
         c->ws_bytes = 0;
         HIPCHK(c, hipMalloc(&c->ws, nd * sizeof(double)));
@@ -669,6 +686,8 @@ void vtk_ctx_destroy(vtk_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    prof_flush(c);
+    for (auto e : c->prof_pool) (void)hipEventDestroy(e);
     (void)hipFree(c->d_part);
     (void)hipFree(c->d_scal);
     (void)hipFree(c->d_state);

@@ -132,7 +132,8 @@ struct SpmvIn {
     const double *x, *halo;   // halo may be null (world == 1)
 };
 
-enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2, EPI_RESID_PREC = 3 };
+// EPI_PREC_DC: w = M^-1 A p_j plus the DCGS2 step's dot products (launch_spmv_dc)
+enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2, EPI_RESID_PREC = 3, EPI_PREC_DC = 4 };
 
 // y = A x (PLAIN); y = b - A x, part0 = sum y^2 (RESID); y = M^-1 A x with M = BJ(inv, bs)
 // or identity (inv == null), part0 = sum y^2, part1 = sum v0*y (PREC, v0 may be null);
@@ -185,6 +186,11 @@ hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, i
 // per-quantity finalize (one workgroup per quantity), single-lane scalar step, update pass.
 hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, int64_t n,
                           double *part, int grid, const int *stop_col, int col, hipStream_t s);
+// DCGS2 step j fused into the SpMV: w = M^-1 A p_j with p_j = V[j] (in.x), and per workgroup
+// the partials of s = V_j^T p_j, z = V_j^T w, |p|^2, p.w, |w|^2 (layout of launch_dc_dots);
+// grid = tiles->grid partials.  BJ-fused tiles with bs in {1, 2, 4, 8} only.
+hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
+                          int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, double *scal,
                               const int *stop_col, int col, hipStream_t s);
 // part != null: reduce the G partials in-kernel (one GPU); else read the all-reduced scal

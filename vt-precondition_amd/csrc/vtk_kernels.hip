@@ -95,6 +95,10 @@ struct SpmvK {
     double *part0, *part1;
     const int *stop_col;
     int col;
+    const double *V;   // EPI_PREC_DC: basis, leading dimension, step, partials
+    int64_t ld;
+    int j;
+    double *dcpart;
 };
 
 template <typename VT, bool HALO>
@@ -118,17 +122,101 @@ __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]
     }
 }
 
-// EPI: 0 plain, 1 residual, 2 preconditioned (BS == 0: identity, else block-Jacobi of size BS)
+// Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
+// 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
+// contiguous id range; with the grid-stride tile loop an XCD then works on a contiguous window
+// of tiles at a time and neighbouring tiles' x halos (+-nv rows on the 2D operator) hit its L2.
+// Speed only: the partial of workgroup b stays at index b, every mapping is fixed.
+__device__ __forceinline__ int xcd_swizzle(int b, int g) {
+    constexpr int NX = 8;
+    const int q = g / NX, r = g % NX, x = b % NX;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / NX;
+}
+
+// DCGS2 dots of rows [i0, i1) of a tile, w and p staged in LDS (wt, pt): wave wv owns the basis
+// vectors k = wv, wv + 4, ...; W = 2: 16-byte loads of V (the tile's first row even)
+constexpr int DC_KPW = DC_MAXJ / (NT / 64);
+struct DcAcc {
+    double s[DC_KPW], z[DC_KPW], aa, ab, ag;
+};
+template <int W>
+__device__ __forceinline__ void dc_rows(DcAcc &d, const double *vb, int64_t ld, int j, const double *pt,
+                                        const double *wt, int nr, int lane, int wv) {
+    for (int i = W * lane; i < nr; i += W * 64) {
+        const bool two = W == 2 && i + 1 < nr;
+        double pv[2], wv2[2];
+        pv[0] = pt[i]; wv2[0] = wt[i];
+        pv[1] = two ? pt[i + 1] : 0.0; wv2[1] = two ? wt[i + 1] : 0.0;
+#pragma unroll
+        for (int u = 0; u < DC_KPW; ++u) {
+            const int k = wv + u * (NT / 64);
+            if (k < j) {
+                const double *vk = vb + (size_t)k * ld + i;
+                double v0, v1 = 0.0;
+                if (two) {
+                    const double2 t = *reinterpret_cast<const double2 *>(vk);
+                    v0 = t.x; v1 = t.y;
+                } else {
+                    v0 = vk[0];
+                }
+                d.s[u] += v0 * pv[0];
+                d.z[u] += v0 * wv2[0];
+                if (W == 2) { d.s[u] += v1 * pv[1]; d.z[u] += v1 * wv2[1]; }
+            }
+        }
+        if (wv == 0) {
+#pragma unroll
+            for (int h = 0; h < W; ++h) {
+                d.aa += pv[h] * pv[h];
+                d.ab += pv[h] * wv2[h];
+                d.ag += wv2[h] * wv2[h];
+            }
+        }
+    }
+}
+
+// per-workgroup partials in launch_dc_dots' layout (part[q * GMAX + block]); red >= DC_NQ doubles
+__device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, double *part) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int u = 0; u < DC_KPW; ++u) {
+        const int k = wv + u * (NT / 64);
+        const double ts = wave_sum(d.s[u]);
+        const double tz = wave_sum(d.z[u]);
+        if (lane == 0 && k < j) { red[k] = ts; red[DC_MAXJ + k] = tz; }
+    }
+    {
+        const double t0 = wave_sum(d.aa), t1 = wave_sum(d.ab), t2 = wave_sum(d.ag);
+        if (wv == 0 && lane == 0) { red[2 * DC_MAXJ] = t0; red[2 * DC_MAXJ + 1] = t1; red[2 * DC_MAXJ + 2] = t2; }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < DC_NQ; q += NT) {
+        const bool used = q < j || (q >= DC_MAXJ && q < DC_MAXJ + j) || q >= 2 * DC_MAXJ;
+        if (used) part[(size_t)q * GMAX + blockIdx.x] = red[q];
+    }
+}
+
+// EPI: 0 plain, 1 residual, 2 preconditioned (BS == 0: identity, else block-Jacobi of size BS),
+// 3 residual + preconditioned, 4 preconditioned + DCGS2 dots
+// 4 waves/SIMD = the LDS-bound occupancy (4 workgroups of 35 KB per CU): caps VGPRs at 128
 template <typename VT, bool HALO, int EPI, int BS>
-__global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_spmv(SpmvK<VT, HALO> a) {
     __shared__ double prod[TILE_NNZ];
     __shared__ int rp[TILE_ROWS + 1];
     __shared__ double red[NT / 64];
+    static_assert(2 * TILE_ROWS <= TILE_NNZ && DC_NQ <= TILE_NNZ, "DC staging in prod[]");
     if (stopped(a.stop_col, a.col)) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    constexpr bool DC = EPI == EPI_PREC_DC;
     double acc0 = 0.0, acc1 = 0.0;
-    for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    DcAcc dc;
+    if constexpr (DC) {
+#pragma unroll
+        for (int u = 0; u < DC_KPW; ++u) { dc.s[u] = 0.0; dc.z[u] = 0.0; }
+        dc.aa = dc.ab = dc.ag = 0.0;
+    }
+    for (int t = xcd_swizzle(blockIdx.x, gridDim.x); t < a.ntiles; t += gridDim.x) {
         const int r0 = a.tile_row[t], r1 = a.tile_row[t + 1], nr = r1 - r0;
         const int nz0 = a.indptr[r0], nnz = a.indptr[r1] - nz0;
         if (nnz <= TILE_NNZ) {
@@ -153,7 +241,11 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
             }
             for (; e < nnz; e += NT) prod[e] = (double)cv[e] * xload(a, ci[e]);
             __syncthreads();
-            for (int base = 0; base < nr; base += NT) {
+            double zk[TILE_ROWS / NT];
+#pragma unroll
+            for (int u = 0; u < TILE_ROWS / NT; ++u) {
+                const int base = u * NT;
+                if (base >= nr) break;
                 const int i = base + tid;
                 const bool act = i < nr;
                 double s = 0.0;
@@ -190,11 +282,12 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
                             if (act) z += m[j] * yj;
                         }
                     }
+                    if constexpr (DC) zk[u] = z;
                     if (act) {
                         a.y[row] = z;
                         if constexpr (EPI == EPI_RESID_PREC) {
                             acc1 += z * z;
-                        } else {
+                        } else if constexpr (!DC) {
                             acc0 += z * z;
                             if (a.v0) acc1 += a.v0[row] * z;
                         }
@@ -202,7 +295,21 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
                 }
             }
             __syncthreads();
-        } else {
+            if constexpr (DC) {
+                // stage the tile's w and p in the (now free) product buffer, then the dots
+                double *wt = prod, *pt = prod + TILE_ROWS;
+#pragma unroll
+                for (int u = 0; u < TILE_ROWS / NT; ++u) {
+                    const int i = u * NT + tid;
+                    if (i < nr) { wt[i] = zk[u]; pt[i] = a.x[r0 + i]; }
+                }
+                __syncthreads();
+                // fused BJ tiles start on a block boundary: even rows for even BS (16-B loads)
+                constexpr int W = (BS >= 2 && BS % 2 == 0) ? 2 : 1;
+                dc_rows<W>(dc, a.V + r0, a.ld, a.j, pt, wt, nr, lane, tid >> 6);
+                __syncthreads();
+            }
+        } else if constexpr (!DC) {   // (DC: BJ-fused tiles never hold long rows)
             // long rows (each such tile is a single row): workgroup-strided products
             for (int i = 0; i < nr; ++i) {
                 const int row = r0 + i;
@@ -231,7 +338,11 @@ __global__ __launch_bounds__(NT) void k_spmv(SpmvK<VT, HALO> a) {
             }
         }
     }
-    if constexpr (EPI != EPI_PLAIN) {
+    if constexpr (DC) {
+        dc_write(dc, a.j, prod, a.dcpart);
+        return;
+    }
+    if constexpr (EPI != EPI_PLAIN && !DC) {
         const double t0 = block_sum(acc0, red);
         if (tid == 0) a.part0[blockIdx.x] = t0;
         if (EPI == EPI_RESID_PREC || (EPI == EPI_PREC && a.v0 != nullptr)) {
@@ -247,7 +358,7 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
                                 double *part1, const int *stop_col, int col, hipStream_t s) {
     SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
                       in.tiles->d_row, in.tiles->ntiles, in.n_local, in.x, in.halo,
-                      y, b, inv, v0, part0, part1, stop_col, col};
+                      y, b, inv, v0, part0, part1, stop_col, col, nullptr, 0, 0, nullptr};
     const dim3 g(in.tiles->grid), blk(NT);
     if (epi == EPI_PLAIN) {
         hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1>), g, blk, 0, s, a);
@@ -279,6 +390,35 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
         }
     }
     return hipGetLastError();
+}
+
+template <typename VT, bool HALO>
+static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
+                                   int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s) {
+    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
+                      in.tiles->d_row, in.tiles->ntiles, in.n_local, in.x, in.halo,
+                      w, nullptr, inv, nullptr, nullptr, nullptr, stop_col, col, V, ld, j, part};
+    const dim3 g(in.tiles->grid), blk(NT);
+    switch (inv ? bs : 0) {   // BJ-fused tiles only; larger blocks would spill (host falls back)
+        case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 1>), g, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 2>), g, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 4>), g, blk, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 8>), g, blk, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
+                          int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s) {
+    if (j > DC_MAXJ || in.tiles->grid > GMAX) return hipErrorInvalidValue;
+    const bool halo = in.halo != nullptr;
+    if (in.fp32) {
+        return halo ? spmv_dc_dispatch<float, true>(in, w, inv, bs, V, ld, j, part, stop_col, col, s)
+                    : spmv_dc_dispatch<float, false>(in, w, inv, bs, V, ld, j, part, stop_col, col, s);
+    }
+    return halo ? spmv_dc_dispatch<double, true>(in, w, inv, bs, V, ld, j, part, stop_col, col, s)
+                : spmv_dc_dispatch<double, false>(in, w, inv, bs, V, ld, j, part, stop_col, col, s);
 }
 
 hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
