@@ -47,6 +47,17 @@ def spmv_bytes(nnz, n, fp32):
     return (8 if fp32 else 12) * nnz + 4 * (n + 1) + 16 * n
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit):
     """SciPy 1.15.3 (the reference scipy.sparse path) on the host cores, bounded sample."""
     import numpy as np
@@ -79,7 +90,7 @@ def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit):
                    f"{cfg_name} operator/RHS, first {s.inner_iters} inner iterations (one restart "
                    f"cycle, legacy maxiter bound) in {s.seconds:.1f} s; csr_matvec is single-threaded, "
                    f"np.dot uses {blas_threads} BLAS threads; host cpus in affinity: "
-                   f"{len(os.sched_getaffinity(0))}"),
+                   f"{len(os.sched_getaffinity(0))}; cpu: {cpu_model()}"),
         "spmv_gbs": spmv_bytes(ip[-1], n, d.dtype == np.float32) / t_spmv / 1e9,
     }
 
@@ -195,6 +206,31 @@ def main():
     t_spmv = ev0.elapsed_time(ev1) / 1e3 / args.spmv_reps
     B = spmv_bytes(A.nnz, A.n_local, fp32)
     spmv_gbs = B / t_spmv / 1e9
+    # cold: median of single reps with the 256 MB Infinity Cache flushed in between
+    flush = torch.empty(512 * 2**20 // 8, dtype=torch.float64, device=dev)
+    cold = []
+    with torch.cuda.stream(stream):
+        for _ in range(min(args.spmv_reps, 20)):
+            flush.fill_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            vk._abi.check(lib.vtk_spmv(A.handle, C.c_void_p(xs.data_ptr()), C.c_void_p(ys.data_ptr()), 1))
+            e1.record(stream)
+            e1.synchronize()
+            cold.append(e0.elapsed_time(e1) / 1e3)
+        # device-copy reference bandwidth: 1 GiB D2D copy (read + write)
+        src = torch.empty(2**27, dtype=torch.float64, device=dev).fill_(1.0)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(5):
+            dst.copy_(src)
+        e1.record(stream)
+        e1.synchronize()
+    copy_gbs = 2 * src.numel() * 8 * 5 / (e0.elapsed_time(e1) / 1e3) / 1e9
+    t_cold = sorted(cold)[len(cold) // 2]
+    del flush, src, dst
 
     # ---- per-kernel profile of one more solve (outside the timed region): HIP events around
     #      every launch on the context's stream, algorithmic bytes per launch
@@ -229,7 +265,9 @@ def main():
         "inner_iters_per_solve": iters / args.steps,
         "info": infos,
         "true_rel_residual": rel_res,
-        "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B},
+        "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B,
+                 "cold_median_us": t_cold * 1e6, "cold_gbs": B / t_cold / 1e9,
+                 "device_copy_gbs": copy_gbs, "frac_of_copy": spmv_gbs / copy_gbs},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": dk["gbs"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": dk["gbs"] / HBM_PEAK_GBS,
                      "traffic": traffic, "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],

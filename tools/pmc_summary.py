@@ -5,12 +5,16 @@
 Reads  <src>/prof/run_kernel_stats.csv            (rocprofv3 --kernel-trace --stats)
        <src>/pmc_fetch/run_counter_collection.csv  (rocprofv3 --pmc FETCH_SIZE)
        <src>/pmc_write/run_counter_collection.csv  (rocprofv3 --pmc WRITE_SIZE)
+       <src>/prof/run_kernel_trace.csv            (per-dispatch durations)
 Writes profiles/<round>_kernel_stats.csv (copy) and profiles/<round>_pmc_traffic.json:
 per kernel the mean FETCH_SIZE / WRITE_SIZE per dispatch (KiB) and the corrected HBM bytes
 per launch, following MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of the bytes of a wide
 coalesced streaming read on gfx950 -> x2; WRITE_SIZE is exact for 16-B/lane stores.  Values
 are per dispatch of the same command, so they compare directly with bench.py's per-launch
 algorithmic bytes.  (Infinity-Cache hits are counted by these counters, not excluded.)
+durations_us: per class the rocprofv3 mean over all dispatches and over the working ones
+(launches past a cycle's stop column exit at entry), the latter comparable with bench.py's
+live HIP-event avg_us.
 """
 import argparse
 import collections
@@ -45,6 +49,16 @@ def load(path):
     return d
 
 
+def trace_durations(path):
+    d = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return d
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", required=True)
@@ -58,16 +72,26 @@ def main():
     ks = os.path.join(src, "prof", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(prof, f"{a.round}_kernel_stats.csv"))
+    durations = trace_durations(os.path.join(src, "prof", "run_kernel_trace.csv"))
     fetch = load(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = load(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
     out = {"_how": ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                     "'python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5'; "
                     "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
                     "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)"),
-           "note": a.note, "kernels": {}}
+           "note": a.note, "kernels": {}, "durations_us": {}}
     for cls, prefix in CLASSES.items():
         fk = [v for k, vs in fetch.items() if k.startswith(prefix) for v in vs]
         wk = [v for k, vs in write.items() if k.startswith(prefix) for v in vs]
+        dur = [v for k, vs in durations.items() if k.startswith(prefix) for v in vs]
+        if dur:
+            # kernels enqueued past a cycle's stop column return at entry (a few us); the
+            # bench's live HIP-event average counts only the working launches
+            cut = 0.05 * max(dur)
+            act = [v for v in dur if v > cut]
+            out["durations_us"][cls] = {"dispatches": len(dur), "mean_all": statistics.mean(dur),
+                                        "working": len(act), "mean_working": statistics.mean(act),
+                                        "early_exit": len(dur) - len(act)}
         if not fk:
             continue
         f_kib, w_kib = statistics.mean(fk), statistics.mean(wk) if wk else 0.0
@@ -79,6 +103,9 @@ def main():
     print("wrote", dst)
     for k, v in out["kernels"].items():
         print(f"  {k:12s} {v['dispatches']:6d} dispatches  {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch")
+    for k, v in out["durations_us"].items():
+        print(f"  {k:12s} {v['working']:4d} working launches {v['mean_working']:9.1f} us "
+              f"(all {v['dispatches']}: {v['mean_all']:.1f} us)")
 
 
 if __name__ == "__main__":
