@@ -124,9 +124,11 @@ void prof_flush(vtk_ctx *c, int last_col = 1 << 30) {
 // world > 1 (equal partial-vector lengths for the in-place all-reduce)
 int grid_for(vtk_ctx *c, int g) { return c->world > 1 ? GMAX : g; }
 
-int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tiles &t) {
+int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tiles &t,
+                 std::vector<int32_t> *rows_out = nullptr) {
     std::vector<int32_t> rows;
     build_tiles(indptr, align, rows, t.has_long, t.aligned);
+    if (rows_out) *rows_out = rows;
     t.ntiles = (int)rows.size() - 1;
     t.align = align;
     t.grid = grid_for(c, std::max(1, std::min(t.ntiles, GMAX)));
@@ -134,6 +136,47 @@ int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tile
     t.d_row = nullptr;
     HIPCHK(c, hipMalloc(&t.d_row, rows.size() * sizeof(int32_t)));
     HIPCHK(c, hipMemcpy(t.d_row, rows.data(), rows.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    return VTK_OK;
+}
+
+void free_tiles(Tiles &t) {
+    (void)hipFree(t.d_row);
+    (void)hipFree(t.d_end);
+    t.d_row = t.d_end = nullptr;
+}
+
+// Split the tiles of `all` (host row boundaries `rows`) into interior tiles (no row reads a halo
+// column) and boundary tiles, as [start, end) lists.  Grids: boundary <= 64 workgroups,
+// interior the rest of GMAX, so both launches' partials fit one GMAX-strided slot row.
+int upload_split_tiles(vtk_ctx *c, const std::vector<int32_t> &rows, const std::vector<uint8_t> &row_halo,
+                       const Tiles &all, Tiles &in, Tiles &bd) {
+    std::vector<int32_t> is, ie, bs_, be;
+    for (size_t t = 0; t + 1 < rows.size(); ++t) {
+        bool h = false;
+        for (int32_t r = rows[t]; r < rows[t + 1] && !h; ++r) h = row_halo[(size_t)r] != 0;
+        (h ? bs_ : is).push_back(rows[t]);
+        (h ? be : ie).push_back(rows[t + 1]);
+    }
+    auto up = [&](const std::vector<int32_t> &st, const std::vector<int32_t> &en, Tiles &t, int gmax) -> int {
+        free_tiles(t);
+        t.ntiles = (int)st.size();
+        t.align = all.align;
+        t.has_long = all.has_long;
+        t.aligned = all.aligned;
+        t.grid = std::max(1, std::min(t.ntiles, gmax));
+        t.nrows = 0;
+        for (size_t k = 0; k < st.size(); ++k) t.nrows += en[k] - st[k];
+        const size_t nb = std::max<size_t>(st.size(), 1) * sizeof(int32_t);
+        HIPCHK(c, hipMalloc(&t.d_row, nb));
+        HIPCHK(c, hipMalloc(&t.d_end, nb));
+        if (!st.empty()) {
+            HIPCHK(c, hipMemcpy(t.d_row, st.data(), st.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+            HIPCHK(c, hipMemcpy(t.d_end, en.data(), en.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        }
+        return VTK_OK;
+    };
+    TRY(up(bs_, be, bd, 64));
+    TRY(up(is, ie, in, GMAX - bd.grid));
     return VTK_OK;
 }
 
@@ -157,23 +200,25 @@ int comm_allreduce(vtk_ctx *c, double *d, int64_t count) {
 // point-to-point exchange: to rank q scnt[q] elements from send+soff[q], from rank q rcnt[q]
 // elements into recv+roff[q] (ncclSend/ncclRecv in one group: xGMI is point-to-point)
 int comm_alltoallv(vtk_ctx *c, const void *send, const std::vector<int64_t> &scnt, const std::vector<int64_t> &soff,
-                   void *recv, const std::vector<int64_t> &rcnt, const std::vector<int64_t> &roff, ncclDataType_t dt, size_t eb) {
+                   void *recv, const std::vector<int64_t> &rcnt, const std::vector<int64_t> &roff, ncclDataType_t dt, size_t eb,
+                   hipStream_t st = nullptr) {
     const int W = c->world;
+    if (!st) st = c->stream;
     if (c->host_comm) {
         const int64_t ns = W ? soff[W - 1] + scnt[W - 1] : 0, nr = W ? roff[W - 1] + rcnt[W - 1] : 0;
         std::vector<char> hs((size_t)std::max<int64_t>(ns, 1) * eb), hr((size_t)std::max<int64_t>(nr, 1) * eb);
-        if (ns) HIPCHK(c, hipMemcpyAsync(hs.data(), send, ns * eb, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (ns) HIPCHK(c, hipMemcpyAsync(hs.data(), send, ns * eb, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
         if (c->hops.alltoallv(c->hops.user, hs.data(), scnt.data(), soff.data(), hr.data(), rcnt.data(), roff.data(), (int64_t)eb) != 0)
             return fail(c, VTK_ERR_STATE, "host alltoallv hook failed");
-        if (nr) HIPCHK(c, hipMemcpyAsync(recv, hr.data(), nr * eb, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (nr) HIPCHK(c, hipMemcpyAsync(recv, hr.data(), nr * eb, hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipStreamSynchronize(st));
         return VTK_OK;
     }
     NCCLCHK(c, ncclGroupStart());
     for (int q = 0; q < W; ++q) {
-        if (scnt[q] > 0) NCCLCHK(c, ncclSend((const char *)send + soff[q] * eb, (size_t)scnt[q], dt, q, c->comm, c->stream));
-        if (rcnt[q] > 0) NCCLCHK(c, ncclRecv((char *)recv + roff[q] * eb, (size_t)rcnt[q], dt, q, c->comm, c->stream));
+        if (scnt[q] > 0) NCCLCHK(c, ncclSend((const char *)send + soff[q] * eb, (size_t)scnt[q], dt, q, c->comm, st));
+        if (rcnt[q] > 0) NCCLCHK(c, ncclRecv((char *)recv + roff[q] * eb, (size_t)rcnt[q], dt, q, c->comm, st));
     }
     NCCLCHK(c, ncclGroupEnd());
     return VTK_OK;
@@ -214,6 +259,22 @@ int halo_exchange(vtk_csr *A, const double *x) {
     return comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble, sizeof(double));
 }
 
+// the same exchange overlapped: pack on the main stream, send/recv on the comm stream;
+// ev_halo marks the halo's arrival (the boundary tiles wait on it)
+int halo_exchange_async(vtk_csr *A, const double *x) {
+    vtk_ctx *c = A->ctx;
+    {
+        Prof pf(c, "halo", -1, 16.0 * A->n_send);
+        HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_pack, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_pack, 0));
+    TRY(comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble,
+                       sizeof(double), c->comm_stream));
+    HIPCHK(c, hipEventRecord(c->ev_halo, c->comm_stream));
+    return VTK_OK;
+}
+
 SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x) {
     return SpmvIn{A->d_indptr, A->d_indices, A->d_data, A->fp32, t, (int)A->n_local, x,
                   A->ctx->world > 1 ? A->d_halo : nullptr};
@@ -236,6 +297,10 @@ int setup_halo(vtk_csr *A) {
                       A->halo_cols.data(), A->recv_cnt.data()) != VTK_OK)
         return fail(c, VTK_ERR_ARG, context_free_error());
     A->n_halo = nh;
+    A->row_halo.assign((size_t)A->n_local, 0);
+    for (int64_t r = 0; r < A->n_local; ++r)
+        for (int32_t k = A->h_indptr[r]; k < A->h_indptr[r + 1]; ++k)
+            if (idx[k] < A->row_begin || idx[k] >= A->row_end) { A->row_halo[(size_t)r] = 1; break; }
     A->recv_off.assign(W, 0);
     for (int q = 1; q < W; ++q) A->recv_off[q] = A->recv_off[q - 1] + A->recv_cnt[q - 1];
     // remap indices on the device
@@ -407,9 +472,28 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     for (int j = 0; j < m; ++j) {
         double *pj = s.V + (size_t)j * s.ld;
         int cnt = 0;
-        if (fused) {
+        const double b_step = b_csr + b_inv + n8 * (j + 2);   // CSR, BJ, p, w, V_j
+        if (fused && s.M->split) {
+            // interior tiles while the halo is in flight, boundary tiles once it has landed;
+            // their partials side by side (cnt = both grids)
+            const Tiles &ti = s.M->tiles_in, &tb = s.M->tiles_bd;
+            TRY(halo_exchange_async(s.A, pj));
+            {
+                SpmvIn in = spmv_in(s.A, &ti, pj);
+                in.halo = nullptr;   // interior tiles read owned columns only
+                Prof pf(c, "spmv_bj_dc", j, b_step * ti.nrows / std::max<double>(1.0, (double)n));
+                HIPCHK(c, launch_spmv_dc(in, s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j, s.dcpart, stop, j, c->stream));
+            }
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+            {
+                Prof pf(c, "spmv_bj_dc_bd", j, b_step * tb.nrows / std::max<double>(1.0, (double)n));
+                HIPCHK(c, launch_spmv_dc(spmv_in(s.A, &tb, pj), s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j,
+                                         s.dcpart + ti.grid, stop, j, c->stream));
+            }
+            cnt = ti.grid + tb.grid;
+        } else if (fused) {
             TRY(halo_exchange(s.A, pj));
-            Prof pf(c, "spmv_bj_dc", j, b_csr + b_inv + n8 * (j + 2));   // CSR, BJ, p, w, V_j
+            Prof pf(c, "spmv_bj_dc", j, b_step);
             HIPCHK(c, launch_spmv_dc(spmv_in(s.A, ft, pj), s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j, s.dcpart,
                                      stop, j, c->stream));
             cnt = ft->grid;
@@ -670,6 +754,9 @@ int vtk_ctx_create(int device, vtk_ctx **out) {
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return bad(e);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e);
+    if ((e = hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking)) != hipSuccess) return bad(e);
+    if ((e = hipEventCreateWithFlags(&c->ev_pack, hipEventDisableTiming)) != hipSuccess) return bad(e);
+    if ((e = hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming)) != hipSuccess) return bad(e);
     if ((e = hipMalloc(&c->d_part, 8 * GMAX * sizeof(double))) != hipSuccess) return bad(e);
     if ((e = hipMalloc(&c->d_scal, 256 * sizeof(double))) != hipSuccess) return bad(e);
     if ((e = hipMalloc(&c->d_state, sizeof(GmresState))) != hipSuccess) return bad(e);
@@ -694,6 +781,10 @@ void vtk_ctx_destroy(vtk_ctx *c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_stop) (void)hipHostFree(c->h_stop);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    if (c->ev_pack) (void)hipEventDestroy(c->ev_pack);
+    if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -929,8 +1020,13 @@ int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (sb != INT32_MAX) return fail(c, VTK_ERR_SINGULAR, "vtk_bjacobi_create: singular diagonal block " + std::to_string(sb + A->row_begin / bs));
     if (pow2) {
-        TRY(upload_tiles(c, A->h_indptr, bs, M->tiles));
+        std::vector<int32_t> rows;
+        TRY(upload_tiles(c, A->h_indptr, bs, M->tiles, &rows));
         M->fused = M->tiles.aligned && !M->tiles.has_long;
+        if (M->fused && c->world > 1 && A->row_halo.size() == (size_t)A->n_local) {
+            TRY(upload_split_tiles(c, rows, A->row_halo, M->tiles, M->tiles_in, M->tiles_bd));
+            M->split = true;
+        }
     }
     *out = M;
     M = nullptr;
@@ -970,7 +1066,9 @@ void vtk_prec_destroy(vtk_prec *M) {
     if (!M) return;
     if (M->A && M->A->ctx) (void)hipSetDevice(M->A->ctx->device);
     (void)hipFree(M->d_inv);
-    (void)hipFree(M->tiles.d_row);
+    free_tiles(M->tiles);
+    free_tiles(M->tiles_in);
+    free_tiles(M->tiles_bd);
     delete M;
 }
 

@@ -55,11 +55,13 @@ struct Red {
 // ---- CSR tiles (CSR-stream row blocks) -----------------------------------------------------
 struct Tiles {
     int32_t *d_row = nullptr;   // tile t = rows [row[t], row[t+1])
+    int32_t *d_end = nullptr;   // optional (split lists): tile t = rows [row[t], end[t])
     int ntiles = 0;
     int align = 1;              // every boundary is a multiple of align (except n_local)
     bool has_long = false;      // some tile is a single row with nnz > TILE_NNZ
     bool aligned = true;        // no align-group had to be split into single-row tiles
     int grid = 0;               // workgroups of the tile kernels = min(ntiles, GMAX)
+    int64_t nrows = 0;          // rows covered (split lists: byte accounting)
 };
 
 }  // namespace vtk
@@ -67,6 +69,8 @@ struct Tiles {
 struct vtk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t comm_stream = nullptr;    // halo exchange overlapped with interior tiles
+    hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     std::string err;
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;            // RCCL (production transport)
@@ -98,6 +102,7 @@ struct vtk_csr {
     int32_t *d_indptr = nullptr, *d_indices = nullptr;  // local column indices
     void *d_data = nullptr;
     std::vector<int32_t> h_indptr;                      // host copy (tile planning)
+    std::vector<uint8_t> row_halo;                      // world > 1: row reads a halo column
     std::vector<int64_t> offsets;                       // partition, world+1
     vtk::Tiles tiles;                                   // align 1
     // halo (world > 1)
@@ -118,6 +123,10 @@ struct vtk_prec {
     double *d_inv = nullptr;     // [nb][bs][bs]
     vtk::Tiles tiles;            // aligned to bs (fused SpMV + BJ)
     bool fused = false;          // fused SpMV+BJ kernel usable
+    // world > 1, fused: the same tiles split into interior (no halo column: run while the halo
+    // exchange is in flight) and boundary tiles (after it lands)
+    vtk::Tiles tiles_in, tiles_bd;
+    bool split = false;
 };
 
 namespace vtk {

@@ -87,7 +87,7 @@ template <typename VT, bool HALO>
 struct SpmvK {
     const int32_t *indptr, *indices;
     const VT *data;
-    const int32_t *tile_row;
+    const int32_t *tile_row, *tile_end;   // tile_end null: tile t ends where t+1 starts
     int ntiles, n_local;
     const double *x, *halo;
     double *y;
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         dc.aa = dc.ab = dc.ag = 0.0;
     }
     for (int t = xcd_swizzle(blockIdx.x, gridDim.x); t < a.ntiles; t += gridDim.x) {
-        const int r0 = a.tile_row[t], r1 = a.tile_row[t + 1], nr = r1 - r0;
+        const int r0 = a.tile_row[t], r1 = a.tile_end ? a.tile_end[t] : a.tile_row[t + 1], nr = r1 - r0;
         const int nz0 = a.indptr[r0], nnz = a.indptr[r1] - nz0;
         if (nnz <= TILE_NNZ) {
             // Plain (cached) loads here: non-temporal 4/8-byte loads ran this kernel 25% slower
@@ -357,7 +357,7 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
                                 const double *inv, int bs, const double *v0, double *part0,
                                 double *part1, const int *stop_col, int col, hipStream_t s) {
     SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
-                      in.tiles->d_row, in.tiles->ntiles, in.n_local, in.x, in.halo,
+                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
                       y, b, inv, v0, part0, part1, stop_col, col, nullptr, 0, 0, nullptr};
     const dim3 g(in.tiles->grid), blk(NT);
     if (epi == EPI_PLAIN) {
@@ -396,7 +396,7 @@ template <typename VT, bool HALO>
 static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
                                    int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s) {
     SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
-                      in.tiles->d_row, in.tiles->ntiles, in.n_local, in.x, in.halo,
+                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
                       w, nullptr, inv, nullptr, nullptr, nullptr, stop_col, col, V, ld, j, part};
     const dim3 g(in.tiles->grid), blk(NT);
     switch (inv ? bs : 0) {   // BJ-fused tiles only; larger blocks would spill (host falls back)
