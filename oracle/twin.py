@@ -266,7 +266,8 @@ def scipy_csr(indptr, indices, data, n):
 
 
 def bj_blocks(indptr, indices, data, n, bs):
-    """Dense diagonal blocks, f64[nb, bs, bs]; a short last block is padded with identity."""
+    """Dense diagonal blocks, f64[nb, bs, bs] (= the blocks of csr_matrix.toarray()); a short last
+    block is padded with identity."""
     nb = (n + bs - 1) // bs
     B = np.zeros((nb, bs, bs), dtype=np.float64)
     ip = np.asarray(indptr, dtype=np.int64)
@@ -274,7 +275,8 @@ def bj_blocks(indptr, indices, data, n, bs):
     cols = np.asarray(indices, dtype=np.int64)
     blk = rows // bs
     m = (cols // bs) == blk
-    B[blk[m], rows[m] % bs, cols[m] % bs] = np.asarray(data, dtype=np.float64)[m]
+    # duplicates (non-canonical CSR) add up in stored order, as csr_matrix.toarray() does
+    np.add.at(B, (blk[m], rows[m] % bs, cols[m] % bs), np.asarray(data, dtype=np.float64)[m])
     tail = n - (nb - 1) * bs
     for t in range(tail, bs):
         B[nb - 1, t, t] = 1.0

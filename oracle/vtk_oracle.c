@@ -170,7 +170,8 @@ int64_t orc_bj_setup(int64_t n, const int32_t *indptr, const int32_t *indices, c
             if (r >= n) { A[i * bs + i] = 1.0; continue; }
             for (int32_t k = indptr[r]; k < indptr[r + 1]; ++k) {
                 int64_t c = indices[k];
-                if (c >= b * bs && c < b * bs + bs) A[i * bs + (c - b * bs)] = val_at(data, fp32, k);
+                /* duplicates add up in stored order (csr_matrix.toarray()) */
+                if (c >= b * bs && c < b * bs + bs) A[i * bs + (c - b * bs)] += val_at(data, fp32, k);
             }
         }
         for (int c = 0; c < bs; ++c) {

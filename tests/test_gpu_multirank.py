@@ -36,7 +36,9 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
     align = p.shape[-1] if p.dim == 2 else (8 if p.dim == 1 else p.shape[-1] * p.shape[-2])
     offs = vk.partition_rows(p.n, world, align)
     rb, re_ = int(offs[rank]), int(offs[rank + 1])
-    if from_host:   # host CSR row block with global columns (vtk_csr_create path)
+    if from_host == "npz":   # this rank's row block of a SciPy archive (vtkrylov.load_npz)
+        A = vk.load_npz(os.path.join(outdir, "A.npz"), ctx=ctx, offsets=offs)
+    elif from_host:   # host CSR row block with global columns (vtk_csr_create path)
         ip, ix, d = coracle.generate(p, rb, re_)
         A = vk.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=ctx, offsets=offs)
     else:           # device assembly of this rank's rows
@@ -57,12 +59,18 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
 
 
 @pytest.mark.parametrize("case,world,from_host,orth", [("S2", 2, False, "mgs"), ("S4", 3, False, "dcgs2"),
-                                                       ("S2", 3, True, "dcgs2"), ("C1", 2, False, "mgs"),
+                                                       ("S2", 3, True, "dcgs2"), ("S4", 2, "npz", "dcgs2"),
+                                                       ("C1", 2, False, "mgs"),
                                                        ("C1", 2, False, "dcgs2")])
 def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 
     from oracle import coracle, twin
+    if from_host == "npz":
+        from vtkrylov import npz
+        p = twin.CONFIGS[case]
+        ip, ix, d = coracle.generate(p)
+        npz.save_npz_arrays(tmp_path / "A.npz", ip, ix, d, (p.n, p.n))
     mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), from_host, orth), nprocs=world, join=True)
     p = twin.CONFIGS[case]
     ip, ix, d = coracle.generate(p)

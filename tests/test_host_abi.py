@@ -133,3 +133,19 @@ def test_halo_plan_matches_reference(vk_lib, name, world):
         xe = np.concatenate([x[rb:re_], x[cols]])
         yl = coracle.spmv(lip.astype(np.int32), loc.astype(np.int32), d[ip[rb]:ip[re_]], xe)
         assert np.array_equal(yl, y[rb:re_])
+
+
+def test_library_is_current():
+    """The in-tree libvtkrylov.so travels to the GPU box as built here: it must not be older
+    than any of its sources (rebuild with `make -C vt-precondition_amd/csrc`)."""
+    import glob
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "vt-precondition_amd", "vtkrylov", "lib", "libvtkrylov.so")
+    if not os.path.exists(so):
+        import pytest
+        pytest.skip("library not built yet")
+    srcs = glob.glob(os.path.join(root, "vt-precondition_amd", "csrc", "*.[hc]*")) + \
+        [os.path.join(root, "include", "vtkrylov.h")]
+    stale = [s for s in srcs if os.path.getmtime(s) > os.path.getmtime(so)]
+    assert not stale, f"libvtkrylov.so is older than {stale}"

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(NT) void k_bj_setup(const int32_t *__restrict__ ind
                 const int64_t c = indices[k] - c0;
                 const double v = (double)data[k];
 #pragma unroll
-                for (int j = 0; j < BS; ++j) if (c == j) A[j] = v;
+                for (int j = 0; j < BS; ++j) if (c == j) A[j] = A[j] + v;   // duplicates add (toarray)
             }
         }
     }
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(NT) void k_bj_setup_generic(const int32_t *__restri
         if (row >= n) { A[i * bs + i] = 1.0; continue; }
         for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
             const int64_t c = indices[k] - blk * bs;
-            if (c >= 0 && c < bs) A[i * bs + c] = (double)data[k];
+            if (c >= 0 && c < bs) A[i * bs + c] = A[i * bs + c] + (double)data[k];
         }
     }
     for (int c = 0; c < bs; ++c) {

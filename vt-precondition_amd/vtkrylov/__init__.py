@@ -24,7 +24,7 @@ import numpy as np
 from . import _abi
 from ._abi import check, lib
 
-__all__ = ["Context", "default_context", "csr_matrix", "vlasov_operator", "block_jacobi",
+__all__ = ["Context", "default_context", "csr_matrix", "load_npz", "save_npz", "vlasov_operator", "block_jacobi",
            "gmres", "VlasovParams", "vlasov_params", "rhs_splitmix", "partition_rows",
            "halo_plan", "device_count", "SolveStats"]
 
@@ -224,9 +224,8 @@ def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> 
     global column indices (multi-GPU); otherwise the whole matrix."""
     ctx = ctx or default_context()
     if hasattr(arg, "tocsr"):
+        # stored order kept: csr_matvec sums each row in stored order, so must the device
         m = arg.tocsr()
-        if not m.has_sorted_indices:
-            m = m.sorted_indices()
         data, indices, indptr = m.data, m.indices, m.indptr
         shape = m.shape
     else:
@@ -244,6 +243,32 @@ def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> 
                                int(indptr[-1]), _np_ptr(indptr), _np_ptr(indices), _np_ptr(data),
                                int(fp32), _abi.PTR_HOST, C.byref(h)), ctx.handle)
     return CsrOperator(h, ctx, fp32)
+
+
+def load_npz(file, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
+    """``scipy.sparse.load_npz`` for CSR archives, straight to the device: with ``offsets``
+    (world+1 row boundaries) each rank reads only its row block (``ctx.rank``)."""
+    from .npz import load_npz_arrays
+    ctx = ctx or default_context()
+    rows = None
+    if offsets is not None:
+        offs = np.asarray(offsets, dtype=np.int64)
+        if offs.shape != (ctx.world + 1,):
+            raise ValueError("offsets must have world+1 entries")
+        rows = (int(offs[ctx.rank]), int(offs[ctx.rank + 1]))
+    indptr, indices, data, shape = load_npz_arrays(file, rows)
+    return csr_matrix((data, indices, indptr), shape=shape, ctx=ctx, offsets=offsets)
+
+
+def save_npz(file, A: CsrOperator, compressed: bool = True) -> None:
+    """``scipy.sparse.save_npz`` of a whole (single-rank) device operator, entries in stored
+    order; a row-sharded operator is saved per rank with ``npz.save_npz_arrays`` on
+    ``A.download()`` (global column ids) and concatenated by the caller."""
+    from .npz import save_npz_arrays
+    if A.n_local != A.n_global:
+        raise ValueError("save_npz needs the whole matrix on this rank (row-sharded operator)")
+    indptr, indices, data = A.download()
+    save_npz_arrays(file, indptr, indices, data, A.shape, compressed)
 
 
 def vlasov_operator(params: VlasovParams, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
