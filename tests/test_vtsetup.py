@@ -22,6 +22,7 @@ def test_typed_config_and_overrides():
     c = SolverConfig.load()
     assert (c.config, c.dim, c.shape, c.fp32) == ("C3", 2, (25000, 800), False)
     assert (c.rtol, c.atol, c.restart, c.block_size, c.seed) == (1e-8, 0.0, 20, 8, 0x5EED)
+    assert (c.orth, c.operator_file) == ("auto", "")
     c4 = SolverConfig.load(config="C4")
     assert (c4.dim, c4.shape, c4.fp32) == (4, (200, 125, 50, 40), True)
     assert parse_config_spec("1:10000:f64") == (1, (10000,), False)
@@ -54,3 +55,21 @@ def test_step_main_runs_on_gpu(gpu, tmp_path, name):
     ip, ix, d = coracle.generate(p)
     b = twin.rhs(p.n)
     assert np.linalg.norm(b - coracle.spmv(ip, ix, d, step.x)) <= 1e-8 * np.linalg.norm(b)
+
+
+@pytest.mark.gpu
+def test_step_main_solves_npz_archive(gpu, tmp_path):
+    """operator/file: the step solves an externally assembled SciPy archive."""
+    from oracle import coracle, twin
+    from vtkrylov import npz
+    from vtsetup.krylov_precondition import KrylovPrecondition
+    p = twin.CONFIGS["S4"]
+    ip, ix, d = coracle.generate(p)
+    f = tmp_path / "s4.npz"
+    npz.save_npz_arrays(f, ip, ix, d, (p.n, p.n))
+    cfg = SolverConfig.load(config="S4", report=str(tmp_path / "r.json"), operator_file=str(f), orth="mgs")
+    step = KrylovPrecondition(cfg, ctx=gpu)
+    res = step.main()
+    assert res["solve"]["info"] == 0 and res["operator"]["source"] == str(f)
+    ref = coracle.gmres(ip, ix, d, twin.rhs(p.n), coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    assert abs(res["solve"]["inner_iters"] - ref.inner_iters) <= 1

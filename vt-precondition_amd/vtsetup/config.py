@@ -59,6 +59,7 @@ class SolverConfig:
     restart: int
     maxiter: int
     orth: str
+    operator_file: str
     preconditioner: str
     block_size: int
     seed: int
@@ -80,6 +81,7 @@ class SolverConfig:
                   restart=int(t.get_node_value("solver/restart")),
                   maxiter=int(t.get_node_value("solver/maxiter")),
                   orth=t.get_node_value("solver/orth").lower(),
+                  operator_file=t.get_node_value("operator/file"),
                   preconditioner=t.get_node_value("preconditioner/type").lower(),
                   block_size=int(t.get_node_value("preconditioner/block_size")),
                   seed=int(t.get_node_value("rhs/seed"), 0),
@@ -90,6 +92,6 @@ class SolverConfig:
                 setattr(cfg, k, v)
         if cfg.preconditioner not in ("block_jacobi", "none"):
             raise ValueError(f"unknown preconditioner {cfg.preconditioner!r}")
-        if cfg.orth not in ("mgs", "cgs2"):
+        if cfg.orth not in ("auto", "mgs", "dcgs2"):
             raise ValueError(f"unknown orthogonalisation {cfg.orth!r}")
         return cfg

@@ -7,6 +7,7 @@ surface as exceptions that ``test_main`` turns into a return code, as in
 vt_precondition.py:66-79.
 
     python -m vtsetup.krylov_precondition [--config C1] [--xml path] [--report out.json]
+                                          [--operator-file matrix.npz]
 """
 from __future__ import annotations
 
@@ -24,15 +25,19 @@ class KrylovPrecondition:
         self.result = {}
 
     def generate_operator(self):
+        """The config's Vlasov operator assembled on the device, or the SciPy archive named by
+        operator/file (vtkrylov.load_npz)."""
         import vtkrylov as vk
         c = self.cfg
         self.ctx = self.ctx or vk.Context(c.device)
-        if c.orth == "cgs2":
-            self.ctx.set_orth(1)
-        p = vk.vlasov_params(c.dim, c.shape, fp32=c.fp32, **c.physics)
         t = time.perf_counter()
-        self.A = vk.vlasov_operator(p, ctx=self.ctx)
+        if c.operator_file:
+            self.A = vk.load_npz(c.operator_file, ctx=self.ctx)
+        else:
+            p = vk.vlasov_params(c.dim, c.shape, fp32=c.fp32, **c.physics)
+            self.A = vk.vlasov_operator(p, ctx=self.ctx)
         self.result["operator"] = {"n": self.A.n_global, "nnz": self.A.nnz,
+                                   "source": c.operator_file or f"vlasov {c.config}",
                                    "t_assemble_s": time.perf_counter() - t}
 
     def setup_preconditioner(self):
@@ -49,7 +54,7 @@ class KrylovPrecondition:
         c = self.cfg
         self.b = vk.rhs_splitmix(self.A.n_global, seed=c.seed)
         self.x, info = vk.gmres(self.A, self.b, rtol=c.rtol, atol=c.atol, restart=c.restart,
-                                maxiter=c.maxiter or None, M=self.M)
+                                maxiter=c.maxiter or None, M=self.M, orth=c.orth)
         st = vk.last_stats()
         self.result["solve"] = {"info": info, "inner_iters": st.inner_iters,
                                 "restarts": st.restarts, "rnorm": st.rnorm, "bnorm": st.bnorm,
@@ -76,9 +81,10 @@ def test_main(argv=None) -> int:
     ap.add_argument("--xml", default=DEFAULT_XML)
     ap.add_argument("--config")
     ap.add_argument("--report")
+    ap.add_argument("--operator-file", help="SciPy save_npz CSR archive to solve")
     a = ap.parse_args(argv)
     try:
-        cfg = SolverConfig.load(a.xml, config=a.config, report=a.report)
+        cfg = SolverConfig.load(a.xml, config=a.config, report=a.report, operator_file=a.operator_file)
         res = KrylovPrecondition(cfg).main()
         print(json.dumps(res))
         return 0 if res["solve"]["info"] == 0 else 1
