@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--orth", default="auto", choices=["auto", "mgs", "dcgs2"],
                     help="orthogonalisation: auto (library default: dcgs2 for restart <= 32), "
                          "mgs (SciPy's sequence) or dcgs2 (one reduction per step)")
+    ap.add_argument("--bj-mode", default="auto", choices=["auto", "inverse", "tridiag"],
+                    help="block-Jacobi apply: auto (tridiagonal-block LU factors when every block is "
+                         "tridiagonal, as on the Vlasov operators), inverse (bit-exact inv*r), tridiag")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     args = ap.parse_args()
@@ -148,7 +151,7 @@ def main():
     offsets = vk.partition_rows(n_glob, world, align) if world > 1 else None
     t0 = time.time()
     A = vk.vlasov_operator(params, ctx=ctx, offsets=offsets)
-    M = vk.block_jacobi(A, args.bs)
+    M = vk.block_jacobi(A, args.bs, mode=args.bj_mode)
     b_host = vk.rhs_splitmix(n_glob, r0=A.row_begin, r1=A.row_end)
     b = torch.from_numpy(b_host).to(dev)
     torch.cuda.synchronize()
@@ -260,7 +263,8 @@ def main():
         "config": {"workload": f"{args.config}: GMRES({args.restart}, {args.orth})+BJ({args.bs}) to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "bs": args.bs, "rtol": args.rtol, "orth": args.orth, "parallelism": f"row-slab x{world}",
+                   "bs": args.bs, "bj_apply": M.mode, "rtol": args.rtol, "orth": args.orth,
+                   "parallelism": f"row-slab x{world}",
                    "comm": args.comm if world > 1 else None},
         "inner_iters_per_solve": iters / args.steps,
         "info": infos,

@@ -55,11 +55,20 @@ typedef enum { VTK_PTR_HOST = 0, VTK_PTR_DEVICE = 1 } vtk_ptr_kind;
 
 typedef enum {
     VTK_ORTH_MGS = 0,   /* modified Gram-Schmidt, SciPy's sequence (iterative.py:755-759):
-                           j+2 dependent reductions per Arnoldi step (default)              */
+                           j+2 dependent reductions per Arnoldi step                        */
     VTK_ORTH_DCGS2 = 1, /* delayed classical GS with re-orthogonalisation: ONE reduction and
                            two passes over the basis per step; restart <= 32                */
     VTK_ORTH_AUTO = 2   /* default: DCGS2 when restart <= 32, else MGS (stats.orth reports) */
 } vtk_orth;
+
+/* How the block-Jacobi preconditioner is applied (same M^-1 either way):                   */
+typedef enum {
+    VTK_BJ_AUTO = 0,    /* default: TRIDIAG when available, else INVERSE                      */
+    VTK_BJ_INVERSE = 1, /* z_b = inv_b r_b, serial row dots: bit-identical to the oracle      */
+    VTK_BJ_TRIDIAG = 2  /* every diagonal block tridiagonal (bs 2/4/8): LU factors, 24 B/row
+                           instead of 8 bs B/row; equal to INVERSE to rounding (factors are
+                           checked against the inverse to 1e-10 at setup)                    */
+} vtk_bj_mode;
 
 /* Synthetic Vlasov operator parameters. */
 typedef struct {
@@ -158,6 +167,11 @@ int vtk_bjacobi_create(vtk_csr *A, int block_size, vtk_prec **out);
 /* export the block inverses: (n_local + bs - 1) / bs blocks of bs*bs doubles, row-major */
 int vtk_bjacobi_inverse(vtk_prec *M, double *inv, int ptr_kind);
 int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int ptr_kind);
+/* select the apply (vtk_bj_mode) for vtk_bjacobi_apply and vtk_gmres; VTK_ERR_ARG if TRIDIAG
+ * is asked for blocks that are not tridiagonal (or whose factors failed the check) */
+int vtk_bjacobi_set_mode(vtk_prec *M, int mode);
+/* *mode_in_use = VTK_BJ_INVERSE or VTK_BJ_TRIDIAG; *tridiag_available = 0/1 (either may be NULL) */
+int vtk_bjacobi_get_mode(vtk_prec *M, int *mode_in_use, int *tridiag_available);
 void vtk_prec_destroy(vtk_prec *M);
 
 /* ---- solver --------------------------------------------------------------------------- */

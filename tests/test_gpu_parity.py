@@ -123,7 +123,8 @@ def test_spmv_ragged_and_long_rows(gpu, vk_lib, golden):
 def test_bj_setup_and_apply_bitexact(ops, golden, name):
     p, A, (ip, ix, d) = ops[name]
     import vtkrylov as vk
-    M = vk.block_jacobi(A, 8)
+    M = vk.block_jacobi(A, 8, mode="inverse")
+    assert M.mode == "inverse"
     inv = coracle.bj_setup(ip, ix, d, 8)
     assert np.array_equal(M.inverse(), inv)
     b = twin.rhs(p.n)
@@ -135,6 +136,25 @@ def test_bj_setup_and_apply_bitexact(ops, golden, name):
         np.testing.assert_allclose(M.inverse(), golden[f"{name}/bj8_inv"], rtol=1e-12, atol=1e-14)
 
 
+@pytest.mark.parametrize("name", SMALL + ["C1"])
+@pytest.mark.parametrize("bs", [2, 4, 8])
+def test_bj_tridiag_apply(ops, name, bs):
+    """The Vlasov operators' diagonal blocks are tridiagonal (v-direction coupling): "auto"
+    applies M^-1 with their LU factors; equal to the oracle's inverse apply to rounding."""
+    p, A, (ip, ix, d) = ops[name]
+    import vtkrylov as vk
+    M = vk.block_jacobi(A, bs)
+    assert M.tridiag_available and M.mode == "tridiag"
+    inv = coracle.bj_setup(ip, ix, d, bs)
+    assert np.array_equal(M.inverse(), inv)          # the inverse is still built (and exported)
+    b = twin.rhs(p.n)
+    ref = coracle.bj_apply(inv, b)
+    z = M @ b
+    np.testing.assert_allclose(z, ref, rtol=1e-12, atol=1e-14 * np.abs(ref).max())
+    M.set_mode("inverse")
+    assert M.mode == "inverse" and np.array_equal(M @ b, ref)
+
+
 @pytest.mark.parametrize("bs", [4, 7, 16])
 def test_bj_ragged_block_sizes(gpu, vk_lib, golden, bs):
     vk = vk_lib
@@ -142,6 +162,10 @@ def test_bj_ragged_block_sizes(gpu, vk_lib, golden, bs):
     n = ip.shape[0] - 1
     A = vk.csr_matrix((d, ix, ip), shape=(n, n), ctx=gpu)
     M = vk.block_jacobi(A, bs)
+    assert M.mode == "inverse"                       # ragged blocks are not tridiagonal
+    if bs in (2, 4, 8):
+        with pytest.raises(ValueError):
+            M.set_mode("tridiag")
     inv = coracle.bj_setup(ip, ix, d, bs)
     assert np.array_equal(M.inverse(), inv)
     b = twin.rhs(n)

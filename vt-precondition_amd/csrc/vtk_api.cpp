@@ -120,6 +120,26 @@ void prof_flush(vtk_ctx *c, int last_col = 1 << 30) {
     c->prof_pending.clear();
 }
 
+// the BJ operator the kernels apply (vtk_bj_mode): tridiagonal factors when available and not
+// switched off, else the inverse rows; null M: identity
+BjOp bj_op(const vtk_prec *M) {
+    BjOp o;
+    if (!M) return o;
+    o.inv = M->d_inv;
+    o.bs = M->bs;
+    if (M->tri_ok && M->mode != VTK_BJ_INVERSE) {
+        o.tri = M->d_tri;
+        o.tri_ld = M->tri_ld;
+    }
+    return o;
+}
+
+// algorithmic bytes per row of one BJ application
+double bj_row_bytes(const vtk_prec *M) {
+    if (!M) return 0.0;
+    return bj_op(M).tri ? 24.0 : 8.0 * M->bs;
+}
+
 // reducing-kernel grid: a function of the local size on one GPU; GMAX on every rank when
 // world > 1 (equal partial-vector lengths for the in-place all-reduce)
 int grid_for(vtk_ctx *c, int g) { return c->world > 1 ? GMAX : g; }
@@ -405,23 +425,23 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
     const double *v0 = want_dots ? s.V : nullptr;
     const double n8 = 8.0 * s.n;
     const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (s.n + 1);
-    const double b_inv = s.M ? 8.0 * s.M->bs * s.n : 0.0;
+    const double b_inv = bj_row_bytes(s.M) * s.n;
     int cnt;
     if (!s.M) {
         Prof pf(c, "spmv_w", col, b_csr + 3 * n8);
-        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PREC, w, nullptr, nullptr, 0, v0, s.part[0], s.part[1], stop, col, c->stream));
+        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PREC, w, nullptr, BjOp{}, v0, s.part[0], s.part[1], stop, col, c->stream));
         cnt = A->tiles.grid;
     } else if (s.M->fused) {
         Prof pf(c, "spmv_bj", col, b_csr + b_inv + 3 * n8);   // x, v0, w + CSR + BJ rows
-        HIPCHK(c, launch_spmv(spmv_in(A, &s.M->tiles, v), EPI_PREC, w, nullptr, s.M->d_inv, s.M->bs, v0, s.part[0], s.part[1], stop, col, c->stream));
+        HIPCHK(c, launch_spmv(spmv_in(A, &s.M->tiles, v), EPI_PREC, w, nullptr, bj_op(s.M), v0, s.part[0], s.part[1], stop, col, c->stream));
         cnt = s.M->tiles.grid;
     } else {
         {
             Prof pf(c, "spmv", col, b_csr + 2 * n8);
-            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, nullptr, 0, nullptr, nullptr, nullptr, stop, col, c->stream));
+            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr, nullptr, stop, col, c->stream));
         }
         Prof pf(c, "bj_apply", col, b_inv + 3 * n8);
-        HIPCHK(c, launch_bj_apply(s.M->d_inv, s.M->bs, s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
+        HIPCHK(c, launch_bj_apply(bj_op(s.M), s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
         cnt = s.G;
     }
     int rc = VTK_OK;
@@ -447,7 +467,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const bool fused = s.M && s.M->fused && s.M->bs <= 8;
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = (s.A->fp32 ? 8.0 : 12.0) * s.A->nnz + 4.0 * (n + 1);
-    const double b_inv = s.M ? 8.0 * s.M->bs * n : 0.0;
+    const double b_inv = bj_row_bytes(s.M) * n;
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
     auto reduce_step = [&](int j, const double *w, int tag, int cnt) -> int {
         if (cnt == 0) {
@@ -482,19 +502,19 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 SpmvIn in = spmv_in(s.A, &ti, pj);
                 in.halo = nullptr;   // interior tiles read owned columns only
                 Prof pf(c, "spmv_bj_dc", j, b_step * ti.nrows / std::max<double>(1.0, (double)n));
-                HIPCHK(c, launch_spmv_dc(in, s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j, s.dcpart, stop, j, c->stream));
+                HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             }
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
             {
                 Prof pf(c, "spmv_bj_dc_bd", j, b_step * tb.nrows / std::max<double>(1.0, (double)n));
-                HIPCHK(c, launch_spmv_dc(spmv_in(s.A, &tb, pj), s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j,
+                HIPCHK(c, launch_spmv_dc(spmv_in(s.A, &tb, pj), s.w, bj_op(s.M), s.V, s.ld, j,
                                          s.dcpart + ti.grid, stop, j, c->stream));
             }
             cnt = ti.grid + tb.grid;
         } else if (fused) {
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
-            HIPCHK(c, launch_spmv_dc(spmv_in(s.A, ft, pj), s.w, s.M->d_inv, s.M->bs, s.V, s.ld, j, s.dcpart,
+            HIPCHK(c, launch_spmv_dc(spmv_in(s.A, ft, pj), s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart,
                                      stop, j, c->stream));
             cnt = ft->grid;
         } else {
@@ -564,7 +584,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     int rc;
     const double n8 = 8.0 * n;
     const double b_spmv = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 2 * n8;
-    const double b_pc = M ? 8.0 * M->bs * n + 2 * n8 : 2 * n8;
+    const double b_pc = bj_row_bytes(M) * n + 2 * n8;
     // ||b|| and ||M b|| (iterative.py:708, :714)
     { Prof pf(c, "dot", -1, n8);
       HIPCHK(c, launch_dot(b, nullptr, n, s.part[0], s.G, c->stream)); }
@@ -572,7 +592,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     TRY(rc);
     HIPCHK(c, launch_finalize(rb, &ds->scal[0], 1, c->stream));
     { Prof pf(c, "bj_apply", -1, b_pc);
-      HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream)); }
+      HIPCHK(c, launch_bj_apply(bj_op(M), n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream)); }
     Red rmb = reduce(c, s.part[1], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rmb, &ds->scal[1], 1, c->stream));
@@ -589,8 +609,8 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         int rc2;
         Red rr;
         if (fres) {
-            Prof pf(c, "spmv_resid_bj", -1, b_csr + (M ? 8.0 * M->bs * n : 0.0) + 3 * n8);
-            HIPCHK(c, launch_spmv(spmv_in(A, rtiles, x), EPI_RESID_PREC, s.V, b, M ? M->d_inv : nullptr, M ? M->bs : 0,
+            Prof pf(c, "spmv_resid_bj", -1, b_csr + bj_row_bytes(M) * n + 3 * n8);
+            HIPCHK(c, launch_spmv(spmv_in(A, rtiles, x), EPI_RESID_PREC, s.V, b, bj_op(M),
                                   nullptr, prr, prz, nullptr, 0, c->stream));
             rr = reduce(c, prr, rtiles->grid, rc2);
             TRY(rc2);
@@ -598,7 +618,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             TRY(rc2);
         } else {
             Prof pf(c, "spmv_resid", -1, b_spmv + n8);
-            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, nullptr, 0, nullptr, prr, nullptr, nullptr, 0, c->stream));
+            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, BjOp{}, nullptr, prr, nullptr, nullptr, 0, c->stream));
             rr = reduce(c, prr, A->tiles.grid, rc2);
             TRY(rc2);
         }
@@ -646,7 +666,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         Red rv = rz;
         if (!fres) {
             { Prof pf(c, "bj_apply", -1, b_pc);
-              HIPCHK(c, launch_bj_apply(M ? M->d_inv : nullptr, M ? M->bs : 1, n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
+              HIPCHK(c, launch_bj_apply(bj_op(M), n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
             rv = reduce(c, s.part[0], s.G, rc);
             TRY(rc);
         }
@@ -986,7 +1006,7 @@ int vtk_spmv(vtk_csr *A, const double *x, double *y, int kind) {
     TRY(halo_exchange(A, sx.d));
     {
         Prof pf(c, "spmv", -1, (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (A->n_local + 1) + 16.0 * A->n_local);
-        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, sx.d), EPI_PLAIN, sy.d, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, c->stream));
+        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, sx.d), EPI_PLAIN, sy.d, nullptr, BjOp{}, nullptr, nullptr, nullptr, nullptr, 0, c->stream));
     }
     if (c->prof_on) prof_flush(c);
     if (kind == VTK_PTR_HOST) {
@@ -1019,6 +1039,24 @@ int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
     HIPCHK(c, hipMemcpyAsync(&sb, sing.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (sb != INT32_MAX) return fail(c, VTK_ERR_SINGULAR, "vtk_bjacobi_create: singular diagonal block " + std::to_string(sb + A->row_begin / bs));
+    if (bs == 2 || bs == 4 || bs == 8) {
+        // tridiagonal blocks (the v-direction coupling of the Vlasov operators): LU factors
+        M->tri_ld = std::max<int64_t>(M->nb, 1) * bs;
+        HIPCHK(c, hipMalloc(&M->d_tri, 3 * M->tri_ld * sizeof(double)));
+        DBuf flags;
+        TRY(dalloc(c, flags, sizeof(int)));
+        HIPCHK(c, hipMemsetAsync(flags.p, 0, sizeof(int), c->stream));
+        HIPCHK(c, launch_bj_tri_setup(A->d_indptr, A->d_indices, A->d_data, A->fp32, A->n_local, bs, M->d_inv,
+                                      M->d_tri, M->tri_ld, flags.as<int>(), c->stream));
+        int fl = 0;
+        HIPCHK(c, hipMemcpyAsync(&fl, flags.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        M->tri_ok = fl == 0;
+        if (!M->tri_ok) {
+            (void)hipFree(M->d_tri);
+            M->d_tri = nullptr;
+        }
+    }
     if (pow2) {
         std::vector<int32_t> rows;
         TRY(upload_tiles(c, A->h_indptr, bs, M->tiles, &rows));
@@ -1052,7 +1090,7 @@ int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
     TRY(stage_in(c, kind == VTK_PTR_DEVICE ? z : nullptr, n, kind, sz));
     {
         Prof pf(c, "bj_apply", -1, 8.0 * M->bs * n + 16.0 * n);
-        HIPCHK(c, launch_bj_apply(M->d_inv, M->bs, n, sr.d, sz.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0, c->stream));
+        HIPCHK(c, launch_bj_apply(bj_op(M), n, sr.d, sz.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0, c->stream));
     }
     if (c->prof_on) prof_flush(c);
     if (kind == VTK_PTR_HOST) {
@@ -1062,10 +1100,29 @@ int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
     return VTK_OK;
 }
 
+int vtk_bjacobi_set_mode(vtk_prec *M, int mode) {
+    if (!M) return VTK_ERR_ARG;
+    vtk_ctx *c = M->A->ctx;
+    if (mode != VTK_BJ_AUTO && mode != VTK_BJ_INVERSE && mode != VTK_BJ_TRIDIAG)
+        return fail(c, VTK_ERR_ARG, "vtk_bjacobi_set_mode: unknown mode");
+    if (mode == VTK_BJ_TRIDIAG && !M->tri_ok)
+        return fail(c, VTK_ERR_ARG, "vtk_bjacobi_set_mode: blocks are not tridiagonal (bs 2/4/8) or their factors failed the check");
+    M->mode = mode;
+    return VTK_OK;
+}
+
+int vtk_bjacobi_get_mode(vtk_prec *M, int *mode_in_use, int *tridiag_available) {
+    if (!M) return VTK_ERR_ARG;
+    if (mode_in_use) *mode_in_use = bj_op(M).tri ? VTK_BJ_TRIDIAG : VTK_BJ_INVERSE;
+    if (tridiag_available) *tridiag_available = M->tri_ok ? 1 : 0;
+    return VTK_OK;
+}
+
 void vtk_prec_destroy(vtk_prec *M) {
     if (!M) return;
     if (M->A && M->A->ctx) (void)hipSetDevice(M->A->ctx->device);
     (void)hipFree(M->d_inv);
+    (void)hipFree(M->d_tri);
     free_tiles(M->tiles);
     free_tiles(M->tiles_in);
     free_tiles(M->tiles_bd);

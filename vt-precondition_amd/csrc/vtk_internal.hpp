@@ -127,6 +127,11 @@ struct vtk_prec {
     // exchange is in flight) and boundary tiles (after it lands)
     vtk::Tiles tiles_in, tiles_bd;
     bool split = false;
+    // tridiagonal blocks: LU factors l | m | g (SoA, stride tri_ld = nb * bs), vtk_bj_mode
+    double *d_tri = nullptr;
+    int64_t tri_ld = 0;
+    bool tri_ok = false;
+    int mode = VTK_BJ_AUTO;
 };
 
 namespace vtk {
@@ -141,19 +146,35 @@ struct SpmvIn {
     const double *x, *halo;   // halo may be null (world == 1)
 };
 
+// block-Jacobi operator as the kernels see it: inverse rows f64[nb][bs][bs], or (tri != null)
+// the LU factors of tridiagonal blocks, SoA l | m | g with stride tri_ld (vtk_api.cpp, BJ
+// modes).  bs == 0: identity.
+struct BjOp {
+    const double *inv = nullptr;
+    const double *tri = nullptr;
+    int64_t tri_ld = 0;
+    int bs = 0;
+};
+
 // EPI_PREC_DC: w = M^-1 A p_j plus the DCGS2 step's dot products (launch_spmv_dc)
 enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2, EPI_RESID_PREC = 3, EPI_PREC_DC = 4 };
 
 // y = A x (PLAIN); y = b - A x, part0 = sum y^2 (RESID); y = M^-1 A x with M = BJ(inv, bs)
 // or identity (inv == null), part0 = sum y^2, part1 = sum v0*y (PREC, v0 may be null);
 // RESID_PREC: r = b - A x, y = M^-1 r, part0 = sum r^2, part1 = sum y^2.
-hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
-                       int bs, const double *v0, double *part0, double *part1,
+hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const BjOp &bj,
+                       const double *v0, double *part0, double *part1,
                        const int *stop_col, int col, hipStream_t s);
 // z = M^-1 r (BJ or identity when inv == null); part0 = sum z^2, part1 = sum v0*z (optional)
-hipError_t launch_bj_apply(const double *inv, int bs, int64_t n, const double *r, double *z,
+hipError_t launch_bj_apply(const BjOp &bj, int64_t n, const double *r, double *z,
                            const double *v0, double *part0, double *part1, int grid,
                            const int *stop_col, int col, hipStream_t s);
+// factors of tridiagonal diagonal blocks (bs in {2, 4, 8}): tri[i] = l_i, tri[ld + i] = m_i = 1/u_i,
+// tri[2 ld + i] = g_i = sup_i m_i (Thomas, no pivoting); *flags |= 1 a block is not tridiagonal,
+// 2 a pivot is tiny, 4 the factors disagree with the Gauss-Jordan inverse beyond 1e-10
+hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
+                               int64_t n, int bs, const double *inv, double *tri, int64_t ld, int *flags,
+                               hipStream_t s);
 hipError_t launch_bj_setup(const int32_t *indptr, const int32_t *indices, const void *data,
                            int fp32, int64_t n, int bs, double *inv, int *d_singular,
                            double *work, hipStream_t s);
@@ -198,7 +219,7 @@ hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, i
 // DCGS2 step j fused into the SpMV: w = M^-1 A p_j with p_j = V[j] (in.x), and per workgroup
 // the partials of s = V_j^T p_j, z = V_j^T w, |p|^2, p.w, |w|^2 (layout of launch_dc_dots);
 // grid = tiles->grid partials.  BJ-fused tiles with bs in {1, 2, 4, 8} only.
-hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
+hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const BjOp &bj, const double *V,
                           int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, double *scal,
                               const int *stop_col, int col, hipStream_t s);

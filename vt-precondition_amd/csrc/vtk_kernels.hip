@@ -95,6 +95,8 @@ struct SpmvK {
     double *part0, *part1;
     const int *stop_col;
     int col;
+    const double *tri;   // TRI: l | m | g factors of tridiagonal blocks, stride tri_ld
+    int64_t tri_ld;
     const double *V;   // EPI_PREC_DC: basis, leading dimension, step, partials
     int64_t ld;
     int j;
@@ -120,6 +122,42 @@ __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]
 #pragma unroll
         for (int j = 0; j < BS; ++j) m[j] = irow[j];
     }
+}
+
+// Block-Jacobi apply with tridiagonal blocks, BS lanes per block (one row each): the LU solve
+// L d = y, U z = d as two affine scans over the group (log2 BS shuffle steps each):
+//   d_i = y_i - l_i d_{i-1},   z_i = m_i d_i - g_i z_{i+1}   (m_i = 1/u_i, g_i = sup_i / u_i)
+// Same M^-1 as the inverse rows to rounding; 24 B per row instead of 8 BS.
+template <int BS>
+__device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, int lane, const double *tri,
+                                               int64_t ld) {
+    const int ii = lane & (BS - 1);
+    double l = 0.0, m = 1.0, g = 0.0;
+    if (act) {
+        l = tri[row];
+        m = tri[ld + row];
+        g = tri[2 * ld + row];
+    }
+    double A = y, B = -l;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double Ap = __shfl_up(A, off, BS), Bp = __shfl_up(B, off, BS);
+        if (ii >= off) {
+            A = A + B * Ap;
+            B = B * Bp;
+        }
+    }
+    A = m * A;
+    B = -g;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double An = __shfl_down(A, off, BS), Bn = __shfl_down(B, off, BS);
+        if (ii + off < BS) {
+            A = A + B * An;
+            B = B * Bn;
+        }
+    }
+    return A;
 }
 
 // Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
@@ -199,7 +237,7 @@ __device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, dou
 // EPI: 0 plain, 1 residual, 2 preconditioned (BS == 0: identity, else block-Jacobi of size BS),
 // 3 residual + preconditioned, 4 preconditioned + DCGS2 dots
 // 4 waves/SIMD = the LDS-bound occupancy (4 workgroups of 35 KB per CU): caps VGPRs at 128
-template <typename VT, bool HALO, int EPI, int BS>
+template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_spmv(SpmvK<VT, HALO> a) {
     __shared__ double prod[TILE_NNZ];
     __shared__ int rp[TILE_ROWS + 1];
@@ -270,7 +308,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         acc0 += sv * sv;
                     }
                     double z = sv;
-                    if constexpr (BS > 0) {
+                    if constexpr (BS > 0 && TRI) {
+                        z = bj_tri_group<BS>(sv, act, row, lane, a.tri, a.tri_ld);
+                    } else if constexpr (BS > 0) {
                         // z_i = sum_j inv[i][j] * y_j over the BS lanes of this block
                         double m[BS];
                         if (act) load_inv_row<BS>(a.inv + (size_t)row * BS, m);
@@ -352,86 +392,94 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 }
 
-template <typename VT, bool HALO>
-static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const double *b,
-                                const double *inv, int bs, const double *v0, double *part0,
-                                double *part1, const int *stop_col, int col, hipStream_t s) {
-    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
-                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
-                      y, b, inv, v0, part0, part1, stop_col, col, nullptr, 0, 0, nullptr};
-    const dim3 g(in.tiles->grid), blk(NT);
-    if (epi == EPI_PLAIN) {
-        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1>), g, blk, 0, s, a);
-    } else if (epi == EPI_RESID) {
-        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID, 1>), g, blk, 0, s, a);
-    } else if (epi == EPI_PREC) {
-        if (inv == nullptr) bs = 0;
+// BJ variants: bs 0 (identity), 1..32 inverse rows, 2/4/8 tridiagonal factors; MAXBS bounds
+// the instantiations (the DCGS2-fused kernel stops at 8: larger blocks spill)
+template <typename VT, bool HALO, int EPI, int MAXBS>
+static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, dim3 g, hipStream_t s) {
+    const dim3 blk(NT);
+    if (tri) {
         switch (bs) {
-            case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 0>), g, blk, 0, s, a); break;
-            case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 1>), g, blk, 0, s, a); break;
-            case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 2>), g, blk, 0, s, a); break;
-            case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 4>), g, blk, 0, s, a); break;
-            case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 8>), g, blk, 0, s, a); break;
-            case 16: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 16>), g, blk, 0, s, a); break;
-            case 32: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC, 32>), g, blk, 0, s, a); break;
+            case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 2, true>), g, blk, 0, s, a); break;
+            case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 4, true>), g, blk, 0, s, a); break;
+            case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 8, true>), g, blk, 0, s, a); break;
             default: return hipErrorInvalidValue;
         }
-    } else {
-        if (inv == nullptr) bs = 0;
-        switch (bs) {
-            case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 0>), g, blk, 0, s, a); break;
-            case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 1>), g, blk, 0, s, a); break;
-            case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 2>), g, blk, 0, s, a); break;
-            case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 4>), g, blk, 0, s, a); break;
-            case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 8>), g, blk, 0, s, a); break;
-            case 16: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 16>), g, blk, 0, s, a); break;
-            case 32: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID_PREC, 32>), g, blk, 0, s, a); break;
-            default: return hipErrorInvalidValue;
-        }
+        return hipGetLastError();
     }
-    return hipGetLastError();
-}
-
-template <typename VT, bool HALO>
-static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
-                                   int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s) {
-    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
-                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
-                      w, nullptr, inv, nullptr, nullptr, nullptr, stop_col, col, V, ld, j, part};
-    const dim3 g(in.tiles->grid), blk(NT);
-    switch (inv ? bs : 0) {   // BJ-fused tiles only; larger blocks would spill (host falls back)
-        case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 1>), g, blk, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 2>), g, blk, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 4>), g, blk, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PREC_DC, 8>), g, blk, 0, s, a); break;
+    switch (bs) {
+        case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 0>), g, blk, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 1>), g, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 2>), g, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 4>), g, blk, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 8>), g, blk, 0, s, a); break;
+        case 16:
+            if constexpr (MAXBS >= 16) { hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 16>), g, blk, 0, s, a); break; }
+            return hipErrorInvalidValue;
+        case 32:
+            if constexpr (MAXBS >= 32) { hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 32>), g, blk, 0, s, a); break; }
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const double *inv, int bs, const double *V,
+template <typename VT, bool HALO>
+static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const double *b, const BjOp &bj,
+                                const double *v0, double *part0, double *part1, const int *stop_col, int col,
+                                hipStream_t s) {
+    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
+                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
+                      y, b, bj.inv, v0, part0, part1, stop_col, col, bj.tri, bj.tri_ld, nullptr, 0, 0, nullptr};
+    const dim3 g(in.tiles->grid), blk(NT);
+    const int bs = (bj.inv || bj.tri) ? bj.bs : 0;
+    const bool tri = bj.tri != nullptr;
+    if (epi == EPI_PLAIN) {
+        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1>), g, blk, 0, s, a);
+        return hipGetLastError();
+    }
+    if (epi == EPI_RESID) {
+        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID, 1>), g, blk, 0, s, a);
+        return hipGetLastError();
+    }
+    if (epi == EPI_PREC) return launch_bj_variant<VT, HALO, EPI_PREC, 32>(a, bs, tri, g, s);
+    return launch_bj_variant<VT, HALO, EPI_RESID_PREC, 32>(a, bs, tri, g, s);
+}
+
+template <typename VT, bool HALO>
+static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, const double *V, int64_t ld,
+                                   int j, double *part, const int *stop_col, int col, hipStream_t s) {
+    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
+                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
+                      w, nullptr, bj.inv, nullptr, nullptr, nullptr, stop_col, col, bj.tri, bj.tri_ld, V, ld, j, part};
+    // BJ-fused tiles only (bs 1..8); the host falls back to the unfused dots otherwise
+    const int bs = (bj.inv || bj.tri) ? bj.bs : 0;
+    if (bs == 0) return hipErrorInvalidValue;
+    return launch_bj_variant<VT, HALO, EPI_PREC_DC, 8>(a, bs, bj.tri != nullptr, dim3(in.tiles->grid), s);
+}
+
+hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const BjOp &bj, const double *V,
                           int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s) {
     if (j > DC_MAXJ || in.tiles->grid > GMAX) return hipErrorInvalidValue;
     const bool halo = in.halo != nullptr;
     if (in.fp32) {
-        return halo ? spmv_dc_dispatch<float, true>(in, w, inv, bs, V, ld, j, part, stop_col, col, s)
-                    : spmv_dc_dispatch<float, false>(in, w, inv, bs, V, ld, j, part, stop_col, col, s);
+        return halo ? spmv_dc_dispatch<float, true>(in, w, bj, V, ld, j, part, stop_col, col, s)
+                    : spmv_dc_dispatch<float, false>(in, w, bj, V, ld, j, part, stop_col, col, s);
     }
-    return halo ? spmv_dc_dispatch<double, true>(in, w, inv, bs, V, ld, j, part, stop_col, col, s)
-                : spmv_dc_dispatch<double, false>(in, w, inv, bs, V, ld, j, part, stop_col, col, s);
+    return halo ? spmv_dc_dispatch<double, true>(in, w, bj, V, ld, j, part, stop_col, col, s)
+                : spmv_dc_dispatch<double, false>(in, w, bj, V, ld, j, part, stop_col, col, s);
 }
 
-hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const double *inv,
-                       int bs, const double *v0, double *part0, double *part1,
+hipError_t launch_spmv(const SpmvIn &in, int epi, double *y, const double *b, const BjOp &bj,
+                       const double *v0, double *part0, double *part1,
                        const int *stop_col, int col, hipStream_t s) {
     // ntiles == 0 still launches: reducing epilogues must write their (zero) partials
     const bool halo = in.halo != nullptr;
     if (in.fp32) {
-        return halo ? spmv_dispatch<float, true>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s)
-                    : spmv_dispatch<float, false>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s);
+        return halo ? spmv_dispatch<float, true>(in, epi, y, b, bj, v0, part0, part1, stop_col, col, s)
+                    : spmv_dispatch<float, false>(in, epi, y, b, bj, v0, part0, part1, stop_col, col, s);
     }
-    return halo ? spmv_dispatch<double, true>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s)
-                : spmv_dispatch<double, false>(in, epi, y, b, inv, bs, v0, part0, part1, stop_col, col, s);
+    return halo ? spmv_dispatch<double, true>(in, epi, y, b, bj, v0, part0, part1, stop_col, col, s)
+                : spmv_dispatch<double, false>(in, epi, y, b, bj, v0, part0, part1, stop_col, col, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -472,12 +520,132 @@ __global__ __launch_bounds__(NT) void k_bj_apply(const double *__restrict__ inv,
     }
 }
 
-hipError_t launch_bj_apply(const double *inv, int bs, int64_t n, const double *r, double *z,
+// tridiagonal-factor variant: the loop bound is workgroup-uniform so every lane of a block's
+// group takes part in the scans
+template <int BS>
+__global__ __launch_bounds__(NT) void k_bj_apply_tri(const double *__restrict__ tri, int64_t ld, int64_t n,
+                                                     const double *__restrict__ r, double *__restrict__ z,
+                                                     const double *__restrict__ v0, double *part0,
+                                                     double *part1, const int *stop_col, int col) {
+    __shared__ double red[NT / 64];
+    if (stopped(stop_col, col)) return;
+    const int lane = threadIdx.x & 63;
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int64_t i0 = (int64_t)blockIdx.x * NT; i0 < n; i0 += (int64_t)gridDim.x * NT) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool act = i < n;
+        const double v = bj_tri_group<BS>(act ? r[i] : 0.0, act, i, lane, tri, ld);
+        if (act) {
+            z[i] = v;
+            acc0 += v * v;
+            if (v0) acc1 += v0[i] * v;
+        }
+    }
+    if (part0) {
+        const double t0 = block_sum(acc0, red);
+        if (threadIdx.x == 0) part0[blockIdx.x] = t0;
+    }
+    if (part1 && v0) {
+        const double t1 = block_sum(acc1, red);
+        if (threadIdx.x == 0) part1[blockIdx.x] = t1;
+    }
+}
+
+hipError_t launch_bj_apply(const BjOp &bj, int64_t n, const double *r, double *z,
                            const double *v0, double *part0, double *part1, int grid,
                            const int *stop_col, int col, hipStream_t s) {
     if (n == 0 && part0 == nullptr) return hipSuccess;
-    hipLaunchKernelGGL(k_bj_apply, dim3(grid), dim3(NT), 0, s, inv, bs, n, r, z, v0, part0, part1,
-                       stop_col, col);
+    if (bj.tri) {
+        switch (bj.bs) {
+            case 2: hipLaunchKernelGGL(k_bj_apply_tri<2>, dim3(grid), dim3(NT), 0, s, bj.tri, bj.tri_ld, n, r, z, v0, part0, part1, stop_col, col); break;
+            case 4: hipLaunchKernelGGL(k_bj_apply_tri<4>, dim3(grid), dim3(NT), 0, s, bj.tri, bj.tri_ld, n, r, z, v0, part0, part1, stop_col, col); break;
+            case 8: hipLaunchKernelGGL(k_bj_apply_tri<8>, dim3(grid), dim3(NT), 0, s, bj.tri, bj.tri_ld, n, r, z, v0, part0, part1, stop_col, col); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_bj_apply, dim3(grid), dim3(NT), 0, s, bj.bs > 0 ? bj.inv : nullptr, bj.bs > 0 ? bj.bs : 1,
+                       n, r, z, v0, part0, part1, stop_col, col);
+    return hipGetLastError();
+}
+
+// Tridiagonal factors of the diagonal blocks, one thread per block (setup, once).  Duplicates
+// add up (toarray semantics); columns outside [0, n) (halo) are not block entries.  Thomas
+// without pivoting: u_0 = d_0, l_i = a_i / u_{i-1}, u_i = d_i - l_i c_{i-1}; the factors are
+// then checked column by column against the Gauss-Jordan inverse of the same block.
+template <typename VT>
+__global__ __launch_bounds__(NT) void k_bj_tri_setup(const int32_t *__restrict__ indptr,
+                                                     const int32_t *__restrict__ indices,
+                                                     const VT *__restrict__ data, int64_t n, int64_t nb, int bs,
+                                                     const double *__restrict__ inv, double *__restrict__ tri,
+                                                     int64_t ld, int *flags) {
+    constexpr int MB = 8;
+    const int64_t blk = (int64_t)blockIdx.x * NT + threadIdx.x;
+    if (blk >= nb || bs > MB) return;
+    double sub[MB], dia[MB], sup[MB], l[MB], m[MB], g[MB];
+    int bad = 0;
+    const int64_t c0 = blk * bs;
+    for (int i = 0; i < bs; ++i) {
+        const int64_t row = c0 + i;
+        sub[i] = 0.0;
+        sup[i] = 0.0;
+        dia[i] = row >= n ? 1.0 : 0.0;
+        if (row >= n) continue;
+        for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
+            const int64_t col = indices[k];
+            if (col >= n) continue;
+            const int64_t c = col - c0;
+            if (c < 0 || c >= bs) continue;
+            const double v = (double)data[k];
+            if (c == i) dia[i] = dia[i] + v;
+            else if (c == i - 1) sub[i] = sub[i] + v;
+            else if (c == i + 1) sup[i] = sup[i] + v;
+            else bad |= 1;
+        }
+    }
+    double u = dia[0];
+    l[0] = 0.0;
+    for (int i = 0; i < bs; ++i) {
+        if (i > 0) {
+            l[i] = sub[i] / u;
+            u = dia[i] - l[i] * sup[i - 1];
+        }
+        const double scale = __builtin_fabs(sub[i]) + __builtin_fabs(dia[i]) + __builtin_fabs(sup[i]);
+        if (!(__builtin_fabs(u) > 1e-12 * scale)) bad |= 2;
+        m[i] = 1.0 / u;
+        g[i] = sup[i] * m[i];
+    }
+    if (!bad && inv) {
+        double err = 0.0, mag = 0.0;
+        for (int k = 0; k < bs; ++k) {
+            double d[MB];
+            for (int i = 0; i < bs; ++i) d[i] = (i == k ? 1.0 : 0.0) - (i > 0 ? l[i] * d[i - 1] : 0.0);
+            double zn = 0.0;
+            for (int i = bs - 1; i >= 0; --i) {
+                zn = m[i] * d[i] - (i + 1 < bs ? g[i] * zn : 0.0);
+                const double ref = inv[(size_t)(c0 + i) * bs + k];
+                err = fmax(err, __builtin_fabs(zn - ref));
+                mag = fmax(mag, __builtin_fabs(ref));
+            }
+        }
+        if (!(err <= 1e-10 * mag)) bad |= 4;
+    }
+    for (int i = 0; i < bs; ++i) {
+        tri[c0 + i] = l[i];
+        tri[ld + c0 + i] = m[i];
+        tri[2 * ld + c0 + i] = g[i];
+    }
+    if (bad) atomicOr(flags, bad);
+}
+
+hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
+                               int64_t n, int bs, const double *inv, double *tri, int64_t ld, int *flags,
+                               hipStream_t s) {
+    const int64_t nb = (n + bs - 1) / bs;
+    if (nb == 0) return hipSuccess;
+    const dim3 g((unsigned)((nb + NT - 1) / NT));
+    if (fp32) hipLaunchKernelGGL(k_bj_tri_setup<float>, g, dim3(NT), 0, s, indptr, indices, (const float *)data, n, nb, bs, inv, tri, ld, flags);
+    else hipLaunchKernelGGL(k_bj_tri_setup<double>, g, dim3(NT), 0, s, indptr, indices, (const double *)data, n, nb, bs, inv, tri, ld, flags);
     return hipGetLastError();
 }
 
@@ -512,6 +680,7 @@ __global__ __launch_bounds__(NT) void k_bj_setup(const int32_t *__restrict__ ind
         } else {
             const int64_t c0 = blk * BS;
             for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
+                if (indices[k] >= n) continue;   // halo column (local numbering >= n_local)
                 const int64_t c = indices[k] - c0;
                 const double v = (double)data[k];
 #pragma unroll
@@ -577,6 +746,7 @@ __global__ __launch_bounds__(NT) void k_bj_setup_generic(const int32_t *__restri
         I[i * bs + i] = 1.0;
         if (row >= n) { A[i * bs + i] = 1.0; continue; }
         for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
+            if (indices[k] >= n) continue;   // halo column
             const int64_t c = indices[k] - blk * bs;
             if (c >= 0 && c < bs) A[i * bs + c] = A[i * bs + c] + (double)data[k];
         }

@@ -281,11 +281,21 @@ def vlasov_operator(params: VlasovParams, *, ctx: Context | None = None, offsets
     return CsrOperator(h, ctx, bool(params.fp32))
 
 
+BJ_MODES = {"auto": 0, "inverse": 1, "tridiag": 2}
+
+
 class BlockJacobi:
     """Block-Jacobi preconditioner M = blockdiag(A)^-1 (SciPy: a LinearOperator whose matvec
-    applies the bs x bs diagonal-block inverses).  ``vtk_bjacobi_create``."""
+    applies the bs x bs diagonal-block inverses).  ``vtk_bjacobi_create``.
 
-    def __init__(self, A: CsrOperator, bs: int = 8):
+    ``mode``: how M^-1 is applied (same operator either way): "inverse" multiplies by the
+    block inverses (bit-identical to the oracle), "tridiag" solves with the LU factors of
+    tridiagonal blocks (bs 2/4/8; 24 B/row instead of 8*bs), "auto" (default) takes "tridiag"
+    when every block is tridiagonal and its factors pass the setup check."""
+
+    def __init__(self, A: CsrOperator, bs: int = 8, mode: str = "auto"):
+        if mode not in BJ_MODES:
+            raise ValueError(f"mode must be one of {sorted(BJ_MODES)}")
         h = C.c_void_p()
         check(lib().vtk_bjacobi_create(A.handle, int(bs), C.byref(h)), A.ctx.handle)
         self._h = h
@@ -293,6 +303,23 @@ class BlockJacobi:
         self.bs = bs
         self.shape = A.shape
         self.dtype = np.dtype(np.float64)
+        self.set_mode(mode)
+
+    def set_mode(self, mode: str):
+        check(lib().vtk_bjacobi_set_mode(self._h, BJ_MODES[mode]), self.A.ctx.handle)
+
+    @property
+    def mode(self) -> str:
+        """The apply in use: "inverse" or "tridiag"."""
+        m = C.c_int()
+        check(lib().vtk_bjacobi_get_mode(self._h, C.byref(m), None), self.A.ctx.handle)
+        return {1: "inverse", 2: "tridiag"}[m.value]
+
+    @property
+    def tridiag_available(self) -> bool:
+        t = C.c_int()
+        check(lib().vtk_bjacobi_get_mode(self._h, None, C.byref(t)), self.A.ctx.handle)
+        return bool(t.value)
 
     @property
     def handle(self):
@@ -331,8 +358,8 @@ class BlockJacobi:
             pass
 
 
-def block_jacobi(A: CsrOperator, bs: int = 8) -> BlockJacobi:
-    return BlockJacobi(A, bs)
+def block_jacobi(A: CsrOperator, bs: int = 8, mode: str = "auto") -> BlockJacobi:
+    return BlockJacobi(A, bs, mode)
 
 
 @dataclass
