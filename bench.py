@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--bj-mode", default="auto", choices=["auto", "inverse", "tridiag"],
                     help="block-Jacobi apply: auto (tridiagonal-block LU factors when every block is "
                          "tridiagonal, as on the Vlasov operators), inverse (bit-exact inv*r), tridiag")
+    ap.add_argument("--layout", default="auto", choices=["auto", "sell", "csr"],
+                    help="SpMV layout: auto (SELL-64 when its padding is small), sell, csr (CSR-stream tiles)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     args = ap.parse_args()
@@ -151,6 +153,7 @@ def main():
     offsets = vk.partition_rows(n_glob, world, align) if world > 1 else None
     t0 = time.time()
     A = vk.vlasov_operator(params, ctx=ctx, offsets=offsets)
+    A.set_layout(args.layout)
     M = vk.block_jacobi(A, args.bs, mode=args.bj_mode)
     b_host = vk.rhs_splitmix(n_glob, r0=A.row_begin, r1=A.row_end)
     b = torch.from_numpy(b_host).to(dev)
@@ -263,7 +266,7 @@ def main():
         "config": {"workload": f"{args.config}: GMRES({args.restart}, {args.orth})+BJ({args.bs}) to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "bs": args.bs, "bj_apply": M.mode, "rtol": args.rtol, "orth": args.orth,
+                   "bs": args.bs, "bj_apply": M.mode, "layout": A.layout, "rtol": args.rtol, "orth": args.orth,
                    "parallelism": f"row-slab x{world}",
                    "comm": args.comm if world > 1 else None},
         "inner_iters_per_solve": iters / args.steps,

@@ -70,6 +70,14 @@ typedef enum {
                            checked against the inverse to 1e-10 at setup)                    */
 } vtk_bj_mode;
 
+/* Device layout of a CSR operator's SpMV (results are bit-identical in both: every row is
+ * summed serially in stored order, as csr_matvec does):                                     */
+typedef enum {
+    VTK_LAYOUT_AUTO = 0, /* default: SELL when its padding is <= 25 % of nnz, else CSR        */
+    VTK_LAYOUT_CSR = 1,  /* CSR-stream tiles (products staged in LDS, one lane per row)       */
+    VTK_LAYOUT_SELL = 2  /* SELL-64 copy: one wavefront per 64 rows, entries column-major     */
+} vtk_layout;
+
 /* Synthetic Vlasov operator parameters. */
 typedef struct {
     int dim;            /* 1, 2 or 4                                   */
@@ -157,6 +165,10 @@ int vtk_csr_info(vtk_csr *A, int64_t *n_global, int64_t *row_begin, int64_t *row
 /* copy this rank's CSR back (indices GLOBAL), host memory */
 int vtk_csr_download(vtk_csr *A, int32_t *indptr, int32_t *indices, void *data);
 void vtk_csr_destroy(vtk_csr *A);
+/* choose the SpMV layout (vtk_layout); SELL builds the copy on first use (device memory:
+ * 12 B per padded entry, 8 B with f32 values) */
+int vtk_csr_set_layout(vtk_csr *A, int layout);
+int vtk_csr_get_layout(vtk_csr *A, int *layout_in_use);
 
 /* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged
  * internally over RCCL when world > 1).  Bit-identical to csr_matvec (serial row sums). */

@@ -28,6 +28,8 @@ for s in "$@"; do
         benchc2) step benchc2 300 python bench.py --config C2 --steps 3 --warmup 1 --no-cpu-baseline ;;
         benchc1) step benchc1 300 python bench.py --config C1 --steps 5 --warmup 1 --no-cpu-baseline ;;
         benchinv) step benchinv 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bj-mode inverse ;;
+        benchc4csr) step benchc4csr 600 python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 --layout csr ;;
+        benchcsr) step benchcsr 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --layout csr ;;
         benchmgs) step benchmgs 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth mgs ;;
         benchdc) step benchdc 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth dcgs2 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;

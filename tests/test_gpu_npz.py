@@ -20,6 +20,8 @@ def test_messy_archive_spmv_bitexact(gpu, vk_lib, tmp_path, compressed):
     D = vk_lib.load_npz(f, ctx=gpu)
     x = twin.rhs(A.shape[0], seed=0xC0FFEE)
     assert np.array_equal(D @ x, A @ x)
+    D.set_layout("sell" if D.layout == "csr" else "csr")   # the other layout, same bits
+    assert np.array_equal(D @ x, A @ x)
     ip, ix, d = D.download()
     assert np.array_equal(ip, A.indptr) and np.array_equal(ix, A.indices) and np.array_equal(d, A.data)
 

@@ -73,15 +73,22 @@ def test_device_generator_hash_c4(gpu, vk_lib, golden_large):
     assert hashlib.sha256(d.tobytes()).hexdigest() == ref["data"]
 
 
+@pytest.mark.parametrize("layout", ["sell", "csr"])
 @pytest.mark.parametrize("name", SMALL + ["C1"])
-def test_spmv_bitexact(ops, golden, name):
+def test_spmv_bitexact(ops, golden, name, layout):
     p, A, (ip, ix, d) = ops[name]
-    x = twin.rhs(p.n, seed=0xC0FFEE)
-    y = A @ x
-    assert np.array_equal(y, coracle.spmv(ip, ix, d, x))
-    if f"{name}/spmv_y" in golden:      # SciPy csr_matvec
-        assert np.array_equal(y, golden[f"{name}/spmv_y"])
-        assert np.array_equal(A @ np.ones(p.n), golden[f"{name}/ones_y"])
+    assert A.layout == "sell"           # auto: the Vlasov operators pad < 25 %
+    A.set_layout(layout)
+    try:
+        assert A.layout == layout
+        x = twin.rhs(p.n, seed=0xC0FFEE)
+        y = A @ x
+        assert np.array_equal(y, coracle.spmv(ip, ix, d, x))
+        if f"{name}/spmv_y" in golden:      # SciPy csr_matvec
+            assert np.array_equal(y, golden[f"{name}/spmv_y"])
+            assert np.array_equal(A @ np.ones(p.n), golden[f"{name}/ones_y"])
+    finally:
+        A.set_layout("auto")
 
 
 def test_spmv_c1_golden_hash(ops, golden_large):
@@ -89,6 +96,40 @@ def test_spmv_c1_golden_hash(ops, golden_large):
     y = A @ twin.rhs(p.n, seed=0xC0FFEE)
     assert hashlib.sha256(y.tobytes()).hexdigest() == golden_large["C1"]["spmv_y_sha256"]
     assert np.linalg.norm(A @ np.ones(p.n)) == pytest.approx(golden_large["C1"]["A_ones_norm2"], rel=1e-15)
+
+
+def test_spmv_ragged_sell_forced_bitexact(gpu, vk_lib, golden):
+    """SELL sums every row in one lane, long rows included: bit-identical everywhere."""
+    vk = vk_lib
+    ip, ix, d = golden["ragged/indptr"], golden["ragged/indices"], golden["ragged/data"]
+    n = ip.shape[0] - 1
+    A = vk.csr_matrix((d, ix, ip), shape=(n, n), ctx=gpu)
+    assert A.layout == "csr"            # auto: padding too large for SELL
+    A.set_layout("sell")
+    assert A.layout == "sell"
+    x = twin.rhs(n, seed=0xC0FFEE)
+    assert np.array_equal(A @ x, coracle.spmv(ip, ix, d, x))
+    assert np.array_equal(A @ x, golden["ragged/spmv_y"])
+
+
+@pytest.mark.parametrize("layout", ["sell", "csr"])
+@pytest.mark.parametrize("bj_mode", ["tridiag", "inverse"])
+def test_gmres_layouts_c1(ops, layout, bj_mode):
+    p, A, (ip, ix, d) = ops["C1"]
+    import vtkrylov as vk
+    A.set_layout(layout)
+    try:
+        M = vk.block_jacobi(A, 8, mode=bj_mode)
+        b = twin.rhs(p.n)
+        inv = coracle.bj_setup(ip, ix, d, 8)
+        ref = coracle.gmres(ip, ix, d, b, inv, rtol=1e-8)
+        x, info = vk.gmres(A, b, rtol=1e-8, M=M)
+        st = vk.last_stats()
+        assert info == ref.info == 0
+        assert abs(st.inner_iters - ref.inner_iters) <= 1
+        assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) <= 1e-9
+    finally:
+        A.set_layout("auto")
 
 
 def test_spmv_ragged_and_long_rows(gpu, vk_lib, golden):

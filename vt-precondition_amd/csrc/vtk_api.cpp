@@ -295,9 +295,28 @@ int halo_exchange_async(vtk_csr *A, const double *x) {
     return VTK_OK;
 }
 
-SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x) {
-    return SpmvIn{A->d_indptr, A->d_indices, A->d_data, A->fp32, t, (int)A->n_local, x,
-                  A->ctx->world > 1 ? A->d_halo : nullptr};
+SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nullptr) {
+    SpmvIn in{A->d_indptr, A->d_indices, A->d_data, A->fp32, t, (int)A->n_local, x,
+              A->ctx->world > 1 ? A->d_halo : nullptr};
+    if (A->use_sell) {   // SELL-64 layout: the tiles are not used
+        in.sell = &A->sell;
+        in.groups = g ? g : &A->g_all;
+    }
+    return in;
+}
+
+// the fused SpMV + BJ kernels apply: SELL chunks align with any power-of-two bs <= 32; the
+// CSR-stream path needs the BJ tiles aligned and free of long rows
+bool bj_fused(const vtk_prec *M) {
+    if (!M) return false;
+    if (M->A->use_sell) return (M->bs & (M->bs - 1)) == 0 && M->bs <= 32;
+    return M->fused;
+}
+
+// interior / boundary pieces of the fused SpMV (world > 1)
+bool bj_split(const vtk_prec *M) { return M && (M->A->use_sell ? M->A->g_in.grid > 0 : M->split); }
+SpmvIn split_in(vtk_csr *A, vtk_prec *M, const double *x, bool interior) {
+    return interior ? spmv_in(A, &M->tiles_in, x, &A->g_in) : spmv_in(A, &M->tiles_bd, x, &A->g_bd);
 }
 
 // Build the halo plan of a freshly uploaded CSR (indices still GLOBAL on the device), remap
@@ -365,10 +384,101 @@ int setup_halo(vtk_csr *A) {
     return VTK_OK;
 }
 
+void free_sell(vtk_csr *A) {
+    (void)hipFree(A->sell.d_off);
+    (void)hipFree(A->sell.d_col);
+    (void)hipFree(A->sell.d_val);
+    A->sell = Sell{};
+    A->use_sell = false;
+}
+
+// SELL-64 copy of the (local-index) CSR on the device.  only_if_compact: stop after the
+// widths when the padding would exceed 25 % of nnz (AUTO); *built says whether it exists.
+int build_sell(vtk_csr *A, bool only_if_compact, bool *built) {
+    vtk_ctx *c = A->ctx;
+    *built = A->sell.d_col != nullptr;
+    if (*built) return VTK_OK;
+    const int64_t n = A->n_local, nch = (n + 63) / 64;
+    const size_t scan_bytes = std::max<size_t>(sell_scan_bytes(n), 16);
+    DBuf tmp, scan;
+    TRY(dalloc(c, tmp, (size_t)(nch + 1) * sizeof(int64_t)));
+    TRY(dalloc(c, scan, scan_bytes));
+    Sell sl;
+    HIPCHK(c, hipMalloc(&sl.d_off, (size_t)(nch + 1) * sizeof(int64_t)));
+    auto drop = [&]() { (void)hipFree(sl.d_off); (void)hipFree(sl.d_col); (void)hipFree(sl.d_val); };
+    hipError_t e = launch_sell_build(A->d_indptr, A->d_indices, A->d_data, A->fp32, n, sl.d_off, tmp.as<int64_t>(),
+                                     scan.p, scan_bytes, nullptr, nullptr, 0, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&sl.entries, sl.d_off + nch, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { drop(); return fail(c, VTK_ERR_HIP, std::string("SELL build: ") + hipGetErrorString(e)); }
+    if (only_if_compact && (double)sl.entries > 1.25 * (double)A->nnz + 64.0) { drop(); return VTK_OK; }
+    const size_t vb = A->fp32 ? 4 : 8;
+    e = hipMalloc(&sl.d_col, (size_t)std::max<int64_t>(sl.entries, 1) * 4);
+    if (e == hipSuccess) e = hipMalloc(&sl.d_val, (size_t)std::max<int64_t>(sl.entries, 1) * vb);
+    if (e == hipErrorOutOfMemory && only_if_compact) { (void)hipGetLastError(); drop(); return VTK_OK; }
+    if (e == hipSuccess) e = launch_sell_build(A->d_indptr, A->d_indices, A->d_data, A->fp32, n, sl.d_off, nullptr,
+                                               nullptr, 0, sl.d_col, sl.d_val, 1, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { drop(); return fail(c, e == hipErrorOutOfMemory ? VTK_ERR_NOMEM : VTK_ERR_HIP,
+                                              std::string("SELL build: ") + hipGetErrorString(e)); }
+    sl.nch = nch;
+    A->sell = sl;
+    *built = true;
+    return VTK_OK;
+}
+
+int upload_groups(vtk_ctx *c, const std::vector<int32_t> &list, int gmax, Groups &g) {
+    (void)hipFree(g.d_list);
+    g.d_list = nullptr;
+    g.count = (int)list.size();
+    g.grid = std::max(1, std::min(g.count, gmax));
+    HIPCHK(c, hipMalloc(&g.d_list, std::max<size_t>(list.size(), 1) * sizeof(int32_t)));
+    if (!list.empty()) HIPCHK(c, hipMemcpy(g.d_list, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    return VTK_OK;
+}
+
+// groups of 4 chunks (256 rows); world > 1: interior groups (no row reads a halo column) and
+// boundary groups for the overlapped exchange (grids <= 64 and the rest of GMAX)
+int build_groups(vtk_csr *A) {
+    vtk_ctx *c = A->ctx;
+    const int ng = (int)((A->n_local + 255) / 256);
+    A->g_all.count = ng;
+    A->g_all.grid = grid_for(c, std::max(1, std::min(ng, GMAX)));
+    if (c->world > 1 && A->row_halo.size() == (size_t)A->n_local) {
+        std::vector<int32_t> gi, gb;
+        for (int g = 0; g < ng; ++g) {
+            bool h = false;
+            for (int64_t r = 256 * (int64_t)g; r < std::min<int64_t>(A->n_local, 256 * (int64_t)g + 256) && !h; ++r)
+                h = A->row_halo[(size_t)r] != 0;
+            (h ? gb : gi).push_back(g);
+        }
+        TRY(upload_groups(c, gb, 64, A->g_bd));
+        TRY(upload_groups(c, gi, GMAX - A->g_bd.grid, A->g_in));
+    }
+    return VTK_OK;
+}
+
+int apply_layout(vtk_csr *A, int layout) {
+    vtk_ctx *c = A->ctx;
+    if (layout == VTK_LAYOUT_CSR) {
+        free_sell(A);
+    } else {
+        bool built = false;
+        TRY(build_sell(A, layout == VTK_LAYOUT_AUTO, &built));
+        A->use_sell = built;
+        if (built && !A->g_all.grid) TRY(build_groups(A));
+    }
+    A->layout = layout;
+    (void)c;
+    return VTK_OK;
+}
+
 int finish_csr(vtk_csr *A) {
     vtk_ctx *c = A->ctx;
     if (c->world > 1) TRY(setup_halo(A));
     TRY(upload_tiles(c, A->h_indptr, 1, A->tiles));
+    TRY(build_groups(A));
+    TRY(apply_layout(A, VTK_LAYOUT_AUTO));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return VTK_OK;
 }
@@ -399,6 +509,9 @@ void destroy_csr(vtk_csr *A) {
     (void)hipFree(A->d_halo);
     (void)hipFree(A->d_send_idx);
     (void)hipFree(A->d_send_buf);
+    free_sell(A);
+    (void)hipFree(A->g_in.d_list);
+    (void)hipFree(A->g_bd.d_list);
     delete A;
 }
 
@@ -429,12 +542,14 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
     int cnt;
     if (!s.M) {
         Prof pf(c, "spmv_w", col, b_csr + 3 * n8);
-        HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PREC, w, nullptr, BjOp{}, v0, s.part[0], s.part[1], stop, col, c->stream));
-        cnt = A->tiles.grid;
-    } else if (s.M->fused) {
+        const SpmvIn in = spmv_in(A, &A->tiles, v);
+        HIPCHK(c, launch_spmv(in, EPI_PREC, w, nullptr, BjOp{}, v0, s.part[0], s.part[1], stop, col, c->stream));
+        cnt = spmv_grid(in);
+    } else if (bj_fused(s.M)) {
         Prof pf(c, "spmv_bj", col, b_csr + b_inv + 3 * n8);   // x, v0, w + CSR + BJ rows
-        HIPCHK(c, launch_spmv(spmv_in(A, &s.M->tiles, v), EPI_PREC, w, nullptr, bj_op(s.M), v0, s.part[0], s.part[1], stop, col, c->stream));
-        cnt = s.M->tiles.grid;
+        const SpmvIn in = spmv_in(A, &s.M->tiles, v);
+        HIPCHK(c, launch_spmv(in, EPI_PREC, w, nullptr, bj_op(s.M), v0, s.part[0], s.part[1], stop, col, c->stream));
+        cnt = spmv_grid(in);
     } else {
         {
             Prof pf(c, "spmv", col, b_csr + 2 * n8);
@@ -464,7 +579,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // every kernel of step j is tagged j: it returns at entry once stop_col < j
     // SpMV + BJ and the step's dots in one pass for BJ-fused tiles with bs <= 8 (larger blocks
     // would spill the fused kernel's registers)
-    const bool fused = s.M && s.M->fused && s.M->bs <= 8;
+    const bool fused = bj_fused(s.M) && s.M->bs <= 8;
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = (s.A->fp32 ? 8.0 : 12.0) * s.A->nnz + 4.0 * (n + 1);
     const double b_inv = bj_row_bytes(s.M) * n;
@@ -493,30 +608,31 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *pj = s.V + (size_t)j * s.ld;
         int cnt = 0;
         const double b_step = b_csr + b_inv + n8 * (j + 2);   // CSR, BJ, p, w, V_j
-        if (fused && s.M->split) {
+        if (fused && bj_split(s.M)) {
             // interior tiles while the halo is in flight, boundary tiles once it has landed;
             // their partials side by side (cnt = both grids)
-            const Tiles &ti = s.M->tiles_in, &tb = s.M->tiles_bd;
+            SpmvIn in = split_in(s.A, s.M, pj, true), bd = split_in(s.A, s.M, pj, false);
+            in.halo = nullptr;   // interior tiles read owned columns only
+            const double f_in = (s.A->use_sell ? s.A->g_in.count * 256.0 : (double)s.M->tiles_in.nrows) /
+                                std::max<double>(1.0, (double)n);
             TRY(halo_exchange_async(s.A, pj));
             {
-                SpmvIn in = spmv_in(s.A, &ti, pj);
-                in.halo = nullptr;   // interior tiles read owned columns only
-                Prof pf(c, "spmv_bj_dc", j, b_step * ti.nrows / std::max<double>(1.0, (double)n));
+                Prof pf(c, "spmv_bj_dc", j, b_step * std::min(1.0, f_in));
                 HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             }
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
             {
-                Prof pf(c, "spmv_bj_dc_bd", j, b_step * tb.nrows / std::max<double>(1.0, (double)n));
-                HIPCHK(c, launch_spmv_dc(spmv_in(s.A, &tb, pj), s.w, bj_op(s.M), s.V, s.ld, j,
-                                         s.dcpart + ti.grid, stop, j, c->stream));
+                Prof pf(c, "spmv_bj_dc_bd", j, b_step * std::max(0.0, 1.0 - f_in));
+                HIPCHK(c, launch_spmv_dc(bd, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart + spmv_grid(in), stop, j,
+                                         c->stream));
             }
-            cnt = ti.grid + tb.grid;
+            cnt = spmv_grid(in) + spmv_grid(bd);
         } else if (fused) {
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
-            HIPCHK(c, launch_spmv_dc(spmv_in(s.A, ft, pj), s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart,
-                                     stop, j, c->stream));
-            cnt = ft->grid;
+            const SpmvIn in = spmv_in(s.A, ft, pj);
+            HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
+            cnt = spmv_grid(in);
         } else {
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
@@ -599,11 +715,12 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     // r = b - A x (iterative.py:737, :816).  When the BJ tiles allow (or M is the identity) the
     // residual kernel also applies M^-1 and writes v0's direction straight into V[0]: the next
     // cycle's psolve(r) (:742) is then already done.
-    const bool fres = !M || M->fused;
-    const Tiles *rtiles = (M && M->fused) ? &M->tiles : &A->tiles;
+    const bool fres = !M || bj_fused(M);
+    const Tiles *rtiles = (M && bj_fused(M)) ? &M->tiles : &A->tiles;
+    const SpmvIn rin0 = spmv_in(A, rtiles, x), pin0 = spmv_in(A, &A->tiles, x);
     double *prr = c->d_part + 4 * GMAX, *prz = c->d_part + 5 * GMAX;
     const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1);
-    Red rz{prz, rtiles->grid};
+    Red rz{prz, spmv_grid(rin0)};
     auto residual = [&]() -> int {
         TRY(halo_exchange(A, x));
         int rc2;
@@ -612,14 +729,14 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             Prof pf(c, "spmv_resid_bj", -1, b_csr + bj_row_bytes(M) * n + 3 * n8);
             HIPCHK(c, launch_spmv(spmv_in(A, rtiles, x), EPI_RESID_PREC, s.V, b, bj_op(M),
                                   nullptr, prr, prz, nullptr, 0, c->stream));
-            rr = reduce(c, prr, rtiles->grid, rc2);
+            rr = reduce(c, prr, spmv_grid(rin0), rc2);
             TRY(rc2);
-            rz = reduce(c, prz, rtiles->grid, rc2);
+            rz = reduce(c, prz, spmv_grid(rin0), rc2);
             TRY(rc2);
         } else {
             Prof pf(c, "spmv_resid", -1, b_spmv + n8);
             HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, BjOp{}, nullptr, prr, nullptr, nullptr, 0, c->stream));
-            rr = reduce(c, prr, A->tiles.grid, rc2);
+            rr = reduce(c, prr, spmv_grid(pin0), rc2);
             TRY(rc2);
         }
         HIPCHK(c, launch_finalize(rr, &ds->rnorm, 1, c->stream));
@@ -1097,6 +1214,22 @@ int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
         HIPCHK(c, hipMemcpyAsync(z, sz.d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
+    return VTK_OK;
+}
+
+int vtk_csr_set_layout(vtk_csr *A, int layout) {
+    if (!A) return VTK_ERR_ARG;
+    vtk_ctx *c = A->ctx;
+    if (layout != VTK_LAYOUT_AUTO && layout != VTK_LAYOUT_CSR && layout != VTK_LAYOUT_SELL)
+        return fail(c, VTK_ERR_ARG, "vtk_csr_set_layout: unknown layout");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return apply_layout(A, layout);
+}
+
+int vtk_csr_get_layout(vtk_csr *A, int *layout_in_use) {
+    if (!A || !layout_in_use) return VTK_ERR_ARG;
+    *layout_in_use = A->use_sell ? VTK_LAYOUT_SELL : VTK_LAYOUT_CSR;
     return VTK_OK;
 }
 

@@ -64,6 +64,21 @@ struct Tiles {
     int64_t nrows = 0;          // rows covered (split lists: byte accounting)
 };
 
+// SELL-64 copy of a CSR (vtk_kernels.hip k_sell): chunk q = local rows 64q..64q+63
+struct Sell {
+    int64_t *d_off = nullptr;   // [nch+1] entry offsets (multiples of 64)
+    int32_t *d_col = nullptr;   // [entries], -1 = padding
+    void *d_val = nullptr;      // [entries] f64 (C4: f32)
+    int64_t nch = 0, entries = 0;
+};
+
+// groups of 4 SELL chunks (256 rows) a SELL launch covers: all (d_list null) or a list
+struct Groups {
+    int32_t *d_list = nullptr;
+    int count = 0;
+    int grid = 0;               // workgroups = min(count, GMAX), >= 1
+};
+
 }  // namespace vtk
 
 struct vtk_ctx {
@@ -103,6 +118,11 @@ struct vtk_csr {
     void *d_data = nullptr;
     std::vector<int32_t> h_indptr;                      // host copy (tile planning)
     std::vector<uint8_t> row_halo;                      // world > 1: row reads a halo column
+    // SELL-64 layout (vtk_csr_set_layout): built when its padding is small (AUTO) or asked for
+    vtk::Sell sell;
+    bool use_sell = false;
+    int layout = VTK_LAYOUT_AUTO;
+    vtk::Groups g_all, g_in, g_bd;                      // g_in/g_bd: world > 1 (halo overlap)
     std::vector<int64_t> offsets;                       // partition, world+1
     vtk::Tiles tiles;                                   // align 1
     // halo (world > 1)
@@ -141,9 +161,11 @@ struct SpmvIn {
     const int32_t *indptr, *indices;
     const void *data;
     int fp32;
-    const Tiles *tiles;
+    const Tiles *tiles;       // CSR-stream tiles (used when sell/groups are null)
     int n_local;
     const double *x, *halo;   // halo may be null (world == 1)
+    const Sell *sell = nullptr;
+    const Groups *groups = nullptr;
 };
 
 // block-Jacobi operator as the kernels see it: inverse rows f64[nb][bs][bs], or (tri != null)
@@ -155,6 +177,9 @@ struct BjOp {
     int64_t tri_ld = 0;
     int bs = 0;
 };
+
+// workgroups (= partials) of a launch on this input
+inline int spmv_grid(const SpmvIn &in) { return (in.sell && in.groups) ? in.groups->grid : in.tiles->grid; }
 
 // EPI_PREC_DC: w = M^-1 A p_j plus the DCGS2 step's dot products (launch_spmv_dc)
 enum Epi { EPI_PLAIN = 0, EPI_RESID = 1, EPI_PREC = 2, EPI_RESID_PREC = 3, EPI_PREC_DC = 4 };
@@ -172,6 +197,12 @@ hipError_t launch_bj_apply(const BjOp &bj, int64_t n, const double *r, double *z
 // factors of tridiagonal diagonal blocks (bs in {2, 4, 8}): tri[i] = l_i, tri[ld + i] = m_i = 1/u_i,
 // tri[2 ld + i] = g_i = sup_i m_i (Thomas, no pivoting); *flags |= 1 a block is not tridiagonal,
 // 2 a pivot is tiny, 4 the factors disagree with the Gauss-Jordan inverse beyond 1e-10
+// SELL-64 build: phase 0 = chunk widths + scan into off (scan_tmp of sell_scan_bytes(n),
+// tmp64 of nch+1 int64), phase 1 = fill col/val
+hipError_t launch_sell_build(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
+                             int64_t *off, int64_t *tmp64, void *scan_tmp, size_t scan_bytes, int32_t *col,
+                             void *val, int phase, hipStream_t s);
+size_t sell_scan_bytes(int64_t n);
 hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
                                int64_t n, int bs, const double *inv, double *tri, int64_t ld, int *flags,
                                hipStream_t s);

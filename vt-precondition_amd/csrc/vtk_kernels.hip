@@ -101,6 +101,13 @@ struct SpmvK {
     int64_t ld;
     int j;
     double *dcpart;
+    // SELL-64 layout (k_sell): chunk q = rows 64q..64q+63, entry k of row 64q+l at
+    // sell_off[q] + 64k + l, col -1 = padding; groups of 4 chunks (256 rows), optional list
+    const int64_t *sell_off;
+    const int32_t *sell_col;
+    const VT *sell_val;
+    const int32_t *group_list;
+    int ngroups;
 };
 
 template <typename VT, bool HALO>
@@ -234,6 +241,58 @@ __device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, dou
     }
 }
 
+// Epilogue of one row (both layouts): y[row] from the row sum s, per-lane partial sums.  All
+// lanes of the wave call it (the BJ groups exchange values by shuffles); act = a real row.
+// Returns the value written (w for the DCGS2 dots).
+template <typename VT, bool HALO, int EPI, int BS, bool TRI>
+__device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double s, int row, bool act, int lane,
+                                               double &acc0, double &acc1) {
+    constexpr bool DC = EPI == EPI_PREC_DC;
+    if constexpr (EPI == EPI_PLAIN) {
+        if (act) a.y[row] = s;
+        return s;
+    } else if constexpr (EPI == EPI_RESID) {
+        const double r = act ? a.b[row] - s : 0.0;
+        if (act) {
+            a.y[row] = r;
+            acc0 += r * r;
+        }
+        return r;
+    } else {
+        // PREC: z = M^-1 (A x);  RESID_PREC: r = b - A x (iterative.py:816), z = M^-1 r
+        double sv = s;
+        if constexpr (EPI == EPI_RESID_PREC) {
+            sv = act ? a.b[row] - s : 0.0;
+            acc0 += sv * sv;
+        }
+        double z = sv;
+        if constexpr (BS > 0 && TRI) {
+            z = bj_tri_group<BS>(sv, act, row, lane, a.tri, a.tri_ld);
+        } else if constexpr (BS > 0) {
+            // z_i = sum_j inv[i][j] * y_j over the BS lanes of this block
+            double m[BS];
+            if (act) load_inv_row<BS>(a.inv + (size_t)row * BS, m);
+            const int gb = lane & ~(BS - 1);
+            z = 0.0;
+#pragma unroll
+            for (int j = 0; j < BS; ++j) {
+                const double yj = __shfl(sv, gb + j, 64);
+                if (act) z += m[j] * yj;
+            }
+        }
+        if (act) {
+            a.y[row] = z;
+            if constexpr (EPI == EPI_RESID_PREC) {
+                acc1 += z * z;
+            } else if constexpr (!DC) {
+                acc0 += z * z;
+                if (a.v0) acc1 += a.v0[row] * z;
+            }
+        }
+        return act ? z : 0.0;
+    }
+}
+
 // EPI: 0 plain, 1 residual, 2 preconditioned (BS == 0: identity, else block-Jacobi of size BS),
 // 3 residual + preconditioned, 4 preconditioned + DCGS2 dots
 // 4 waves/SIMD = the LDS-bound occupancy (4 workgroups of 35 KB per CU): caps VGPRs at 128
@@ -292,47 +351,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     for (int k = rp[i]; k < k1; ++k) s += prod[k];
                 }
                 const int row = r0 + i;
-                if constexpr (EPI == EPI_PLAIN) {
-                    if (act) a.y[row] = s;
-                } else if constexpr (EPI == EPI_RESID) {
-                    if (act) {
-                        const double r = a.b[row] - s;
-                        a.y[row] = r;
-                        acc0 += r * r;
-                    }
-                } else {
-                    // PREC: z = M^-1 (A x);  RESID_PREC: r = b - A x (iterative.py:816), z = M^-1 r
-                    double sv = s;
-                    if constexpr (EPI == EPI_RESID_PREC) {
-                        sv = act ? a.b[row] - s : 0.0;
-                        acc0 += sv * sv;
-                    }
-                    double z = sv;
-                    if constexpr (BS > 0 && TRI) {
-                        z = bj_tri_group<BS>(sv, act, row, lane, a.tri, a.tri_ld);
-                    } else if constexpr (BS > 0) {
-                        // z_i = sum_j inv[i][j] * y_j over the BS lanes of this block
-                        double m[BS];
-                        if (act) load_inv_row<BS>(a.inv + (size_t)row * BS, m);
-                        const int gb = lane & ~(BS - 1);
-                        z = 0.0;
-#pragma unroll
-                        for (int j = 0; j < BS; ++j) {
-                            const double yj = __shfl(sv, gb + j, 64);
-                            if (act) z += m[j] * yj;
-                        }
-                    }
-                    if constexpr (DC) zk[u] = z;
-                    if (act) {
-                        a.y[row] = z;
-                        if constexpr (EPI == EPI_RESID_PREC) {
-                            acc1 += z * z;
-                        } else if constexpr (!DC) {
-                            acc0 += z * z;
-                            if (a.v0) acc1 += a.v0[row] * z;
-                        }
-                    }
-                }
+                const double z = row_epilogue<VT, HALO, EPI, BS, TRI>(a, s, row, act, lane, acc0, acc1);
+                if constexpr (DC) zk[u] = z;
             }
             __syncthreads();
             if constexpr (DC) {
@@ -392,31 +412,170 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// CSR SpMV in the SELL-64 layout (built on the device from the CSR when its padding is small,
+// vtk_api.cpp): one wavefront per 64-row chunk, lane l = row 64q+l, entries column-major in the
+// chunk.  Every lane sums its row's products serially in stored order (padding skipped), so y
+// is bit-identical to csr_matvec and to k_spmv.  No LDS and no barriers on the SpMV itself; a
+// workgroup takes a group of 4 chunks (256 contiguous rows), which the DCGS2 dots reuse as
+// their tile.  col/val are streamed once: non-temporal loads (tools/probe_sell.hip, C3:
+// 291 us vs 348 us for the CSR-stream tiles, bit-identical).
+// ------------------------------------------------------------------------------------------
+template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_sell(SpmvK<VT, HALO> a) {
+    constexpr int SW = 8;   // entries per load batch
+    constexpr bool DC = EPI == EPI_PREC_DC;
+    __shared__ double stage[2 * NT];          // DC: w | p of the group; then the partials
+    __shared__ double red[NT / 64];
+    static_assert(2 * NT >= DC_NQ, "partials staging");
+    if (stopped(a.stop_col, a.col)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double acc0 = 0.0, acc1 = 0.0;
+    DcAcc dc;
+    if constexpr (DC) {
+#pragma unroll
+        for (int u = 0; u < DC_KPW; ++u) { dc.s[u] = 0.0; dc.z[u] = 0.0; }
+        dc.aa = dc.ab = dc.ag = 0.0;
+    }
+    for (int t = blockIdx.x; t < a.ngroups; t += gridDim.x) {
+        const int g = a.group_list ? a.group_list[t] : t;
+        const int q = 4 * g + wv;
+        const int row = 64 * q + lane;
+        const bool act = row < a.n_local;
+        double s = 0.0;
+        if (64 * q < a.n_local) {
+            const int64_t o0 = a.sell_off[q];
+            const int w = (int)((a.sell_off[q + 1] - o0) >> 6);
+            const int32_t *cc = a.sell_col + o0 + lane;
+            const VT *vv = a.sell_val + o0 + lane;
+            for (int k0 = 0; k0 < w; k0 += SW) {
+                int c[SW];
+                double d[SW];
+#pragma unroll
+                for (int u = 0; u < SW; ++u) {
+                    const bool ok = k0 + u < w;
+                    c[u] = ok ? __builtin_nontemporal_load(cc + (k0 + u) * 64) : -1;
+                    d[u] = ok ? (double)__builtin_nontemporal_load(vv + (k0 + u) * 64) : 0.0;
+                }
+                double xv[SW];
+#pragma unroll
+                for (int u = 0; u < SW; ++u) xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
+#pragma unroll
+                for (int u = 0; u < SW; ++u)
+                    if (c[u] >= 0) s += d[u] * xv[u];
+            }
+        }
+        const double z = row_epilogue<VT, HALO, EPI, BS, TRI>(a, s, row, act, lane, acc0, acc1);
+        if constexpr (DC) {
+            // the group's w and p, then the dots over its rows (16-B loads of V: 256g is even)
+            stage[tid] = z;
+            stage[NT + tid] = act ? a.x[row] : 0.0;
+            __syncthreads();
+            const int r0 = 256 * g;
+            const int nr = min(256, a.n_local - r0);
+            dc_rows<2>(dc, a.V + r0, a.ld, a.j, stage + NT, stage, nr, lane, wv);
+            __syncthreads();
+        }
+    }
+    if constexpr (DC) {
+        dc_write(dc, a.j, stage, a.dcpart);
+        return;
+    }
+    if constexpr (EPI != EPI_PLAIN) {
+        const double t0 = block_sum(acc0, red);
+        if (tid == 0) a.part0[blockIdx.x] = t0;
+        if (EPI == EPI_RESID_PREC || (EPI == EPI_PREC && a.v0 != nullptr)) {
+            const double t1 = block_sum(acc1, red);
+            if (tid == 0) a.part1[blockIdx.x] = t1;
+        }
+    }
+}
+
+// SELL-64 build: chunk q's width = its longest row; offsets = exclusive scan of 64*width
+__global__ __launch_bounds__(NT) void k_sell_width(const int32_t *__restrict__ indptr, int64_t n, int64_t nch,
+                                                   int64_t *__restrict__ w64) {
+    for (int64_t q = (int64_t)blockIdx.x * NT + threadIdx.x; q <= nch; q += (int64_t)gridDim.x * NT) {
+        int w = 0;
+        if (q < nch) {
+            const int64_t r1 = q * 64 + 64 < n ? q * 64 + 64 : n;
+            for (int64_t r = q * 64; r < r1; ++r) w = max(w, indptr[r + 1] - indptr[r]);
+        }
+        w64[q] = 64 * (int64_t)w;   // w64[nch] = 0: the scan's last entry is the total
+    }
+}
+
+template <typename VT>
+__global__ __launch_bounds__(NT) void k_sell_fill(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
+                                                  const VT *__restrict__ data, int64_t n, int64_t nch,
+                                                  const int64_t *__restrict__ off, int32_t *__restrict__ col,
+                                                  VT *__restrict__ val) {
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < nch * 64; r += (int64_t)gridDim.x * NT) {
+        const int64_t q = r >> 6, l = r & 63;
+        const int w = (int)((off[q + 1] - off[q]) >> 6);
+        const int k0 = r < n ? indptr[r] : 0, len = r < n ? indptr[r + 1] - k0 : 0;
+        int32_t *cc = col + off[q] + l;
+        VT *vv = val + off[q] + l;
+        for (int k = 0; k < w; ++k) {
+            cc[(int64_t)k * 64] = k < len ? indices[k0 + k] : -1;
+            vv[(int64_t)k * 64] = k < len ? data[k0 + k] : (VT)0;
+        }
+    }
+}
+
+hipError_t launch_sell_build(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
+                             int64_t *off, int64_t *tmp64, void *scan_tmp, size_t scan_bytes, int32_t *col,
+                             void *val, int phase, hipStream_t s) {
+    const int64_t nch = (n + 63) / 64;
+    if (phase == 0) {   // widths + scan -> off[0..nch]
+        hipLaunchKernelGGL(k_sell_width, dim3(1024), dim3(NT), 0, s, indptr, n, nch, tmp64);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, tmp64, off, (int)(nch + 1), s);
+    }
+    if (fp32) hipLaunchKernelGGL(k_sell_fill<float>, dim3(4096), dim3(NT), 0, s, indptr, indices, (const float *)data, n, nch, off, col, (float *)val);
+    else hipLaunchKernelGGL(k_sell_fill<double>, dim3(4096), dim3(NT), 0, s, indptr, indices, (const double *)data, n, nch, off, col, (double *)val);
+    return hipGetLastError();
+}
+
+size_t sell_scan_bytes(int64_t n) {
+    const int64_t nch = (n + 63) / 64;
+    size_t bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (int64_t *)nullptr, (int64_t *)nullptr, (int)(nch + 1));
+    return bytes;
+}
+
 // BJ variants: bs 0 (identity), 1..32 inverse rows, 2/4/8 tridiagonal factors; MAXBS bounds
-// the instantiations (the DCGS2-fused kernel stops at 8: larger blocks spill)
+// the instantiations (the DCGS2-fused kernel stops at 8: larger blocks spill).  SELL: the
+// SELL-64 kernel, else the CSR-stream tiles.
+#define VTK_SPMV_LAUNCH(EPI_, BS_, TRI_)                                                        \
+    do {                                                                                        \
+        if (sell) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_, BS_, TRI_>), g, blk, 0, s, a);     \
+        else hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_, BS_, TRI_>), g, blk, 0, s, a);          \
+    } while (0)
+
 template <typename VT, bool HALO, int EPI, int MAXBS>
-static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, dim3 g, hipStream_t s) {
+static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, bool sell, dim3 g, hipStream_t s) {
     const dim3 blk(NT);
     if (tri) {
         switch (bs) {
-            case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 2, true>), g, blk, 0, s, a); break;
-            case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 4, true>), g, blk, 0, s, a); break;
-            case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 8, true>), g, blk, 0, s, a); break;
+            case 2: VTK_SPMV_LAUNCH(EPI, 2, true); break;
+            case 4: VTK_SPMV_LAUNCH(EPI, 4, true); break;
+            case 8: VTK_SPMV_LAUNCH(EPI, 8, true); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
     switch (bs) {
-        case 0: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 0>), g, blk, 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 1>), g, blk, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 2>), g, blk, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 4>), g, blk, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 8>), g, blk, 0, s, a); break;
+        case 0: VTK_SPMV_LAUNCH(EPI, 0, false); break;
+        case 1: VTK_SPMV_LAUNCH(EPI, 1, false); break;
+        case 2: VTK_SPMV_LAUNCH(EPI, 2, false); break;
+        case 4: VTK_SPMV_LAUNCH(EPI, 4, false); break;
+        case 8: VTK_SPMV_LAUNCH(EPI, 8, false); break;
         case 16:
-            if constexpr (MAXBS >= 16) { hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 16>), g, blk, 0, s, a); break; }
+            if constexpr (MAXBS >= 16) { VTK_SPMV_LAUNCH(EPI, 16, false); break; }
             return hipErrorInvalidValue;
         case 32:
-            if constexpr (MAXBS >= 32) { hipLaunchKernelGGL((k_spmv<VT, HALO, EPI, 32>), g, blk, 0, s, a); break; }
+            if constexpr (MAXBS >= 32) { VTK_SPMV_LAUNCH(EPI, 32, false); break; }
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
@@ -424,42 +583,62 @@ static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, 
 }
 
 template <typename VT, bool HALO>
+static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, const BjOp &bj, const double *v0,
+                                 double *part0, double *part1, const int *stop_col, int col) {
+    const bool sell = in.sell && in.groups;
+    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
+                      in.tiles ? in.tiles->d_row : nullptr, in.tiles ? in.tiles->d_end : nullptr,
+                      in.tiles ? in.tiles->ntiles : 0, in.n_local, in.x, in.halo,
+                      y, b, bj.inv, v0, part0, part1, stop_col, col, bj.tri, bj.tri_ld, nullptr, 0, 0, nullptr,
+                      sell ? in.sell->d_off : nullptr, sell ? in.sell->d_col : nullptr,
+                      sell ? static_cast<const VT *>(in.sell->d_val) : nullptr,
+                      sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0};
+    return a;
+}
+
+template <typename VT, bool HALO>
 static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const double *b, const BjOp &bj,
                                 const double *v0, double *part0, double *part1, const int *stop_col, int col,
                                 hipStream_t s) {
-    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
-                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
-                      y, b, bj.inv, v0, part0, part1, stop_col, col, bj.tri, bj.tri_ld, nullptr, 0, 0, nullptr};
-    const dim3 g(in.tiles->grid), blk(NT);
+    const SpmvK<VT, HALO> a = spmv_args<VT, HALO>(in, y, b, bj, v0, part0, part1, stop_col, col);
+    const bool sell = in.sell && in.groups;
+    const dim3 g(spmv_grid(in)), blk(NT);
     const int bs = (bj.inv || bj.tri) ? bj.bs : 0;
     const bool tri = bj.tri != nullptr;
     if (epi == EPI_PLAIN) {
-        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1>), g, blk, 0, s, a);
+        // no partials: SELL fills the chip at its 8 waves/SIMD (52 VGPRs) with 2048 workgroups
+        // (tools/probe_sell.hip, C4: 965 us at 2048 vs 1362 us at 1024; C3 within 2 %)
+        const dim3 gp(sell ? (unsigned)std::max(1, std::min(in.groups->count, 2 * GMAX)) : g.x);
+        if (sell) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false>), gp, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1, false>), g, blk, 0, s, a);
         return hipGetLastError();
     }
     if (epi == EPI_RESID) {
-        hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_RESID, 1>), g, blk, 0, s, a);
+        VTK_SPMV_LAUNCH(EPI_RESID, 1, false);
         return hipGetLastError();
     }
-    if (epi == EPI_PREC) return launch_bj_variant<VT, HALO, EPI_PREC, 32>(a, bs, tri, g, s);
-    return launch_bj_variant<VT, HALO, EPI_RESID_PREC, 32>(a, bs, tri, g, s);
+    if (epi == EPI_PREC) return launch_bj_variant<VT, HALO, EPI_PREC, 32>(a, bs, tri, sell, g, s);
+    return launch_bj_variant<VT, HALO, EPI_RESID_PREC, 32>(a, bs, tri, sell, g, s);
 }
 
 template <typename VT, bool HALO>
 static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, const double *V, int64_t ld,
                                    int j, double *part, const int *stop_col, int col, hipStream_t s) {
-    SpmvK<VT, HALO> a{in.indptr, in.indices, static_cast<const VT *>(in.data),
-                      in.tiles->d_row, in.tiles->d_end, in.tiles->ntiles, in.n_local, in.x, in.halo,
-                      w, nullptr, bj.inv, nullptr, nullptr, nullptr, stop_col, col, bj.tri, bj.tri_ld, V, ld, j, part};
+    SpmvK<VT, HALO> a = spmv_args<VT, HALO>(in, w, nullptr, bj, nullptr, nullptr, nullptr, stop_col, col);
+    a.V = V;
+    a.ld = ld;
+    a.j = j;
+    a.dcpart = part;
     // BJ-fused tiles only (bs 1..8); the host falls back to the unfused dots otherwise
     const int bs = (bj.inv || bj.tri) ? bj.bs : 0;
     if (bs == 0) return hipErrorInvalidValue;
-    return launch_bj_variant<VT, HALO, EPI_PREC_DC, 8>(a, bs, bj.tri != nullptr, dim3(in.tiles->grid), s);
+    return launch_bj_variant<VT, HALO, EPI_PREC_DC, 8>(a, bs, bj.tri != nullptr, in.sell && in.groups,
+                                                       dim3(spmv_grid(in)), s);
 }
 
 hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const BjOp &bj, const double *V,
                           int64_t ld, int j, double *part, const int *stop_col, int col, hipStream_t s) {
-    if (j > DC_MAXJ || in.tiles->grid > GMAX) return hipErrorInvalidValue;
+    if (j > DC_MAXJ || spmv_grid(in) > GMAX) return hipErrorInvalidValue;
     const bool halo = in.halo != nullptr;
     if (in.fp32) {
         return halo ? spmv_dc_dispatch<float, true>(in, w, bj, V, ld, j, part, stop_col, col, s)

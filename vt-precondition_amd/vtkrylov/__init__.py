@@ -178,6 +178,19 @@ class CsrOperator:
     def handle(self):
         return self._h
 
+    LAYOUTS = {"auto": 0, "csr": 1, "sell": 2}
+
+    def set_layout(self, layout: str):
+        """SpMV layout: "sell" (SELL-64 copy), "csr" (CSR-stream tiles) or "auto" (SELL when
+        its padding is <= 25 % of nnz).  Results are bit-identical either way."""
+        check(lib().vtk_csr_set_layout(self._h, self.LAYOUTS[layout]), self.ctx.handle)
+
+    @property
+    def layout(self) -> str:
+        v = C.c_int()
+        check(lib().vtk_csr_get_layout(self._h, C.byref(v)), self.ctx.handle)
+        return {1: "csr", 2: "sell"}[v.value]
+
     def matvec(self, x):
         """y = A x on this rank's rows (sparsetools csr_matvec, bit-identical)."""
         vx = _Vec(x, self.n_local)

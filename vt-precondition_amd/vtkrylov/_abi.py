@@ -81,6 +81,8 @@ PROTOTYPES = {
     "vtk_bjacobi_inverse": (C.c_int, [P, P, C.c_int]),
     "vtk_bjacobi_apply": (C.c_int, [P, P, P, C.c_int]),
     "vtk_bjacobi_set_mode": (C.c_int, [P, C.c_int]),
+    "vtk_csr_set_layout": (C.c_int, [P, C.c_int]),
+    "vtk_csr_get_layout": (C.c_int, [P, C.POINTER(C.c_int)]),
     "vtk_bjacobi_get_mode": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_destroy": (None, [P]),
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
