@@ -235,6 +235,15 @@ def main():
         e1.record(stream)
         e1.synchronize()
     copy_gbs = 2 * src.numel() * 8 * 5 / (e0.elapsed_time(e1) / 1e3) / 1e9
+    # device-read reference: a torch reduction over the same 1 GiB (read-only stream)
+    with torch.cuda.stream(stream):
+        src.sum()
+        e0.record(stream)
+        for _ in range(5):
+            src.sum()
+        e1.record(stream)
+        e1.synchronize()
+    read_gbs = src.numel() * 8 * 5 / (e0.elapsed_time(e1) / 1e3) / 1e9
     t_cold = sorted(cold)[len(cold) // 2]
     del flush, src, dst
 
@@ -274,7 +283,8 @@ def main():
         "true_rel_residual": rel_res,
         "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B,
                  "cold_median_us": t_cold * 1e6, "cold_gbs": B / t_cold / 1e9,
-                 "device_copy_gbs": copy_gbs, "frac_of_copy": spmv_gbs / copy_gbs},
+                 "device_copy_gbs": copy_gbs, "frac_of_copy": spmv_gbs / copy_gbs,
+                 "device_read_gbs": read_gbs, "frac_of_read": spmv_gbs / read_gbs},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": dk["gbs"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": dk["gbs"] / HBM_PEAK_GBS,
                      "traffic": traffic, "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],

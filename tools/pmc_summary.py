@@ -24,19 +24,20 @@ import os
 import shutil
 import statistics
 
-CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output
-    "spmv_bj": "void vtk::k_spmv<double, false, 2, 8>",
-    "spmv": "void vtk::k_spmv<double, false, 0, 1>",
-    "spmv_resid": "void vtk::k_spmv<double, false, 1, 1>",
-    "spmv_resid_bj": "void vtk::k_spmv<double, false, 3, 8>",
-    "spmv_bj_dc": "void vtk::k_spmv<double, false, 4, 8>",
+CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output (default path:
+              # SELL-64 layout, tridiagonal-factor BJ(8), DCGS2)
+    "spmv_bj_dc": "void vtk::k_sell<double, false, 4, 8, true>",
+    "spmv": "void vtk::k_sell<double, false, 0, 1, false>",
+    "spmv_resid_bj": "void vtk::k_sell<double, false, 3, 8, true>",
+    "spmv_csr": "void vtk::k_spmv<double, false, 0, 1",
+    "spmv_bj_dc_csr": "void vtk::k_spmv<double, false, 4, 8",
     "dc_dots": "vtk::k_dc_dots(",
     "dc_update": "vtk::k_dc_update(",
     "dc_scalar": "vtk::k_dc_scalar(",
     "mgs": "vtk::k_mgs(",
     "tail": "vtk::k_tail(",
     "xupdate": "vtk::k_xupdate(",
-    "bj_apply": "vtk::k_bj_apply(",
+    "bj_apply": "vtk::k_bj_apply",
     "scale0": "vtk::k_scale0(",
 }
 

@@ -198,8 +198,8 @@ __device__ __forceinline__ void dc_rows(DcAcc &d, const double *vb, int64_t ld, 
             if (k < j) {
                 const double *vk = vb + (size_t)k * ld + i;
                 double v0, v1 = 0.0;
-                if (two) {
-                    const double2 t = *reinterpret_cast<const double2 *>(vk);
+                if (two) {   // streamed once here (re-read by the update pass, not from cache)
+                    const d2v t = ldnt2(vk);
                     v0 = t.x; v1 = t.y;
                 } else {
                     v0 = vk[0];
