@@ -417,25 +417,40 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // vtk_api.cpp): one wavefront per 64-row chunk, lane l = row 64q+l, entries column-major in the
 // chunk.  Every lane sums its row's products serially in stored order (padding skipped), so y
 // is bit-identical to csr_matvec and to k_spmv.  No LDS and no barriers on the SpMV itself; a
-// workgroup takes a group of 4 chunks (256 contiguous rows), which the DCGS2 dots reuse as
-// their tile.  col/val are streamed once: non-temporal loads (tools/probe_sell.hip, C3:
-// 291 us vs 348 us for the CSR-stream tiles, bit-identical).
+// workgroup takes a group of 4 chunks (256 contiguous rows).  col/val are streamed once:
+// non-temporal loads (tools/probe_sell.hip, C3: 291 us vs 348 us for the CSR-stream tiles,
+// bit-identical).
+//
+// DCGS2 dots (EPI_PREC_DC), wave-local: each lane already holds its row's w and p, so the wave
+// reads V[k][row] for every k < j itself (8 loads in flight per batch, no LDS staging, no
+// barrier).  The first DC_JB vectors accumulate per lane in registers and are reduced once at
+// the end; vectors beyond (j > 16) are reduced per chunk with a butterfly (every lane gets the
+// same bits) and lane k keeps their running sums.  C3: the LDS-staged split of the vectors
+// over the waves cost 462 us + 33.4 us per vector, butterflies for every vector 320 us + 68 us.
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_allsum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
 template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_sell(SpmvK<VT, HALO> a) {
     constexpr int SW = 8;   // entries per load batch
+    constexpr int KB = 4;   // basis vectors per load batch (DC)
+    constexpr int JB = 12;  // basis vectors with per-lane register accumulators (DC)
     constexpr bool DC = EPI == EPI_PREC_DC;
-    __shared__ double stage[2 * NT];          // DC: w | p of the group; then the partials
+    constexpr int NQW = 2 * DC_MAXJ + 3;      // per-wave partial record (DC)
+    __shared__ double stage[(NT / 64) * NQW];
     __shared__ double red[NT / 64];
-    static_assert(2 * NT >= DC_NQ, "partials staging");
     if (stopped(a.stop_col, a.col)) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double acc0 = 0.0, acc1 = 0.0;
-    DcAcc dc;
+    double dsl = 0.0, dzl = 0.0, daa = 0.0, dab = 0.0, dag = 0.0;   // DC
+    double as_[DC ? JB : 1], az_[DC ? JB : 1];
     if constexpr (DC) {
 #pragma unroll
-        for (int u = 0; u < DC_KPW; ++u) { dc.s[u] = 0.0; dc.z[u] = 0.0; }
-        dc.aa = dc.ab = dc.ag = 0.0;
+        for (int k = 0; k < JB; ++k) { as_[k] = 0.0; az_[k] = 0.0; }
     }
     for (int t = blockIdx.x; t < a.ngroups; t += gridDim.x) {
         const int g = a.group_list ? a.group_list[t] : t;
@@ -467,18 +482,75 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         const double z = row_epilogue<VT, HALO, EPI, BS, TRI>(a, s, row, act, lane, acc0, acc1);
         if constexpr (DC) {
-            // the group's w and p, then the dots over its rows (16-B loads of V: 256g is even)
-            stage[tid] = z;
-            stage[NT + tid] = act ? a.x[row] : 0.0;
-            __syncthreads();
-            const int r0 = 256 * g;
-            const int nr = min(256, a.n_local - r0);
-            dc_rows<2>(dc, a.V + r0, a.ld, a.j, stage + NT, stage, nr, lane, wv);
-            __syncthreads();
+            const double pv = act ? a.x[row] : 0.0;   // p_j (= the SpMV input) on this row
+            daa += pv * pv;
+            dab += pv * z;
+            dag += z * z;
+            const double *vb = a.V + row;
+#pragma unroll
+            for (int k0 = 0; k0 < JB; k0 += KB) {
+                if (k0 >= a.j) break;   // wave-uniform
+                double v[KB];
+#pragma unroll
+                for (int u = 0; u < KB; ++u)
+                    v[u] = (k0 + u < a.j && act) ? __builtin_nontemporal_load(vb + (size_t)(k0 + u) * a.ld) : 0.0;
+#pragma unroll
+                for (int u = 0; u < KB; ++u) {
+                    as_[k0 + u] += v[u] * pv;
+                    az_[k0 + u] += v[u] * z;
+                }
+            }
+            for (int k0 = JB; k0 < a.j; k0 += KB) {
+                double v[KB];
+#pragma unroll
+                for (int u = 0; u < KB; ++u)
+                    v[u] = (k0 + u < a.j && act) ? __builtin_nontemporal_load(vb + (size_t)(k0 + u) * a.ld) : 0.0;
+#pragma unroll
+                for (int u = 0; u < KB; ++u) {
+                    if (k0 + u < a.j) {   // wave-uniform
+                        const double ts = wave_allsum(v[u] * pv), tz = wave_allsum(v[u] * z);
+                        if (lane == k0 + u) {
+                            dsl += ts;
+                            dzl += tz;
+                        }
+                    }
+                }
+            }
         }
     }
     if constexpr (DC) {
-        dc_write(dc, a.j, stage, a.dcpart);
+        // per-block partials in launch_dc_dots' layout: the 4 waves' records summed in order
+        double *rec = stage + wv * NQW;
+        if (lane >= JB && lane < a.j) {
+            rec[lane] = dsl;
+            rec[DC_MAXJ + lane] = dzl;
+        }
+#pragma unroll
+        for (int k = 0; k < JB; ++k) {
+            if (k < a.j) {   // wave-uniform
+                const double ts = wave_sum(as_[k]), tz = wave_sum(az_[k]);
+                if (lane == 0) {
+                    rec[k] = ts;
+                    rec[DC_MAXJ + k] = tz;
+                }
+            }
+        }
+        const double t0 = wave_sum(daa), t1 = wave_sum(dab), t2 = wave_sum(dag);
+        if (lane == 0) {
+            rec[2 * DC_MAXJ] = t0;
+            rec[2 * DC_MAXJ + 1] = t1;
+            rec[2 * DC_MAXJ + 2] = t2;
+        }
+        __syncthreads();
+        for (int qq = tid; qq < DC_NQ; qq += NT) {
+            const bool used = qq < a.j || (qq >= DC_MAXJ && qq < DC_MAXJ + a.j) || qq >= 2 * DC_MAXJ;
+            if (used) {
+                double t = 0.0;
+#pragma unroll
+                for (int w2 = 0; w2 < NT / 64; ++w2) t += stage[w2 * NQW + qq];
+                a.dcpart[(size_t)qq * GMAX + blockIdx.x] = t;
+            }
+        }
         return;
     }
     if constexpr (EPI != EPI_PLAIN) {
