@@ -115,6 +115,8 @@ def main():
                          "tridiagonal, as on the Vlasov operators), inverse (bit-exact inv*r), tridiag")
     ap.add_argument("--layout", default="auto", choices=["auto", "sell", "csr"],
                     help="SpMV layout: auto (SELL-64 when its padding is small), sell, csr (CSR-stream tiles)")
+    ap.add_argument("--comm-solo", action="store_true",
+                    help="one GPU through the distributed code paths (one-rank RCCL communicator)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     args = ap.parse_args()
@@ -142,6 +144,9 @@ def main():
             vkcomm.init_rccl(ctx, rank, world)
         else:
             vkcomm.init_host(ctx, rank, world)
+    elif args.comm_solo:
+        os.environ["VTK_COMM_SOLO"] = "1"
+        ctx.comm_init(0, 1, vk.Context.unique_id())
     ctx.set_orth(vk._abi.ORTH[args.orth])
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
@@ -277,7 +282,7 @@ def main():
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
                    "bs": args.bs, "bj_apply": M.mode, "layout": A.layout, "rtol": args.rtol, "orth": args.orth,
                    "parallelism": f"row-slab x{world}",
-                   "comm": args.comm if world > 1 else None},
+                   "comm": args.comm if world > 1 else ("rccl-solo" if args.comm_solo else None)},
         "inner_iters_per_solve": iters / args.steps,
         "info": infos,
         "true_rel_residual": rel_res,

@@ -30,6 +30,9 @@ for s in "$@"; do
         benchinv) step benchinv 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bj-mode inverse ;;
         benchc4csr) step benchc4csr 600 python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 --layout csr ;;
         benchcsr) step benchcsr 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --layout csr ;;
+        benchsolo) step benchsolo 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --comm-solo ;;
+        benchc1solo) step benchc1solo 300 python bench.py --config C1 --steps 5 --warmup 1 --no-cpu-baseline --comm-solo ;;
+        gridscan) for G in 512 768 896 960 1000 1024; do VTK_SELL_GRID=$G step grid$G 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; done ;;
         benchmgs) step benchmgs 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth mgs ;;
         benchdc) step benchdc 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth dcgs2 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;

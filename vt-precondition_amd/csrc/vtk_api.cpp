@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -142,7 +143,7 @@ double bj_row_bytes(const vtk_prec *M) {
 
 // reducing-kernel grid: a function of the local size on one GPU; GMAX on every rank when
 // world > 1 (equal partial-vector lengths for the in-place all-reduce)
-int grid_for(vtk_ctx *c, int g) { return c->world > 1 ? GMAX : g; }
+int grid_for(vtk_ctx *c, int g) { return c->dist ? GMAX : g; }
 
 int upload_tiles(vtk_ctx *c, const std::vector<int32_t> &indptr, int align, Tiles &t,
                  std::vector<int32_t> *rows_out = nullptr) {
@@ -264,7 +265,7 @@ int comm_allgather_i64(vtk_ctx *c, const int64_t *send, int64_t *recv, int64_t c
 // all-reduced in place: consumers then sum them exactly as on one GPU, with no extra kernel.
 Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
     rc = VTK_OK;
-    if (c->world > 1) {
+    if (c->dist) {
         Prof pf(c, "allreduce", -1, 8.0 * cnt);
         rc = comm_allreduce(c, part, cnt);
     }
@@ -273,7 +274,7 @@ Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
 
 int halo_exchange(vtk_csr *A, const double *x) {
     vtk_ctx *c = A->ctx;
-    if (c->world == 1) return VTK_OK;
+    if (!c->dist) return VTK_OK;
     Prof pf(c, "halo", -1, 16.0 * A->n_send + 8.0 * A->n_halo);
     HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
     return comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble, sizeof(double));
@@ -297,7 +298,7 @@ int halo_exchange_async(vtk_csr *A, const double *x) {
 
 SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nullptr) {
     SpmvIn in{A->d_indptr, A->d_indices, A->d_data, A->fp32, t, (int)A->n_local, x,
-              A->ctx->world > 1 ? A->d_halo : nullptr};
+              A->ctx->dist ? A->d_halo : nullptr};
     if (A->use_sell) {   // SELL-64 layout: the tiles are not used
         in.sell = &A->sell;
         in.groups = g ? g : &A->g_all;
@@ -444,7 +445,9 @@ int build_groups(vtk_csr *A) {
     const int ng = (int)((A->n_local + 255) / 256);
     A->g_all.count = ng;
     A->g_all.grid = grid_for(c, std::max(1, std::min(ng, GMAX)));
-    if (c->world > 1 && A->row_halo.size() == (size_t)A->n_local) {
+    if (const char *e = std::getenv("VTK_SELL_GRID"); e && !c->dist)   // tuning experiments
+        A->g_all.grid = std::max(1, std::min({ng, GMAX, std::atoi(e)}));
+    if (c->dist && A->row_halo.size() == (size_t)A->n_local) {
         std::vector<int32_t> gi, gb;
         for (int g = 0; g < ng; ++g) {
             bool h = false;
@@ -475,7 +478,7 @@ int apply_layout(vtk_csr *A, int layout) {
 
 int finish_csr(vtk_csr *A) {
     vtk_ctx *c = A->ctx;
-    if (c->world > 1) TRY(setup_halo(A));
+    if (c->dist) TRY(setup_halo(A));
     TRY(upload_tiles(c, A->h_indptr, 1, A->tiles));
     TRY(build_groups(A));
     TRY(apply_layout(A, VTK_LAYOUT_AUTO));
@@ -591,7 +594,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             cnt = s.G;
         }
         const double *part = s.dcpart;
-        if (c->world > 1) {
+        if (c->dist) {
             { Prof pf(c, "dc_finalize", tag, 0.0);
               HIPCHK(c, launch_dc_finalize(s.dcpart, cnt, j, w != nullptr, c->d_scal, stop, tag, c->stream)); }
             Prof pf(c, "allreduce", tag, 8.0 * DC_NQ);
@@ -952,13 +955,18 @@ int vtk_comm_unique_id(void *out128) {
 int vtk_comm_init(vtk_ctx *c, int rank, int world, const void *uid) {
     if (!c || world < 1 || rank < 0 || rank >= world) return fail(c, VTK_ERR_ARG, "vtk_comm_init: bad rank/world");
     HIPCHK(c, hipSetDevice(c->device));
-    if (world == 1) { c->rank = 0; c->world = 1; return VTK_OK; }
+    // world 1: no communicator, unless VTK_COMM_SOLO=1 asks for a one-rank RCCL communicator
+    // that runs every distributed code path (halo plan and exchange, all-reduces, split lists)
+    const char *solo = std::getenv("VTK_COMM_SOLO");
+    const bool force = world == 1 && solo && solo[0] == '1';
+    if (world == 1 && !force) { c->rank = 0; c->world = 1; c->dist = false; return VTK_OK; }
     if (!uid) return fail(c, VTK_ERR_ARG, "vtk_comm_init: unique id required");
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
     NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
     c->rank = rank;
     c->world = world;
+    c->dist = true;
     return VTK_OK;
 }
 
@@ -970,6 +978,7 @@ int vtk_comm_init_host(vtk_ctx *c, int rank, int world, const vtk_host_comm *ops
     c->rank = rank;
     c->world = world;
     c->host_comm = world > 1;
+    c->dist = world > 1;
     if (ops) c->hops = *ops;
     return VTK_OK;
 }
@@ -1178,7 +1187,7 @@ int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
         std::vector<int32_t> rows;
         TRY(upload_tiles(c, A->h_indptr, bs, M->tiles, &rows));
         M->fused = M->tiles.aligned && !M->tiles.has_long;
-        if (M->fused && c->world > 1 && A->row_halo.size() == (size_t)A->n_local) {
+        if (M->fused && c->dist && A->row_halo.size() == (size_t)A->n_local) {
             TRY(upload_split_tiles(c, rows, A->row_halo, M->tiles, M->tiles_in, M->tiles_bd));
             M->split = true;
         }

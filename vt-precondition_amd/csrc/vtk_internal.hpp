@@ -88,6 +88,8 @@ struct vtk_ctx {
     hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     std::string err;
     int rank = 0, world = 1;
+    bool dist = false;                    // distributed code paths: world > 1, or a one-rank
+                                          // RCCL communicator (VTK_COMM_SOLO=1, testing)
     ncclComm_t comm = nullptr;            // RCCL (production transport)
     bool host_comm = false;               // host-staged hooks (vtk_comm_init_host)
     vtk_host_comm hops{};
