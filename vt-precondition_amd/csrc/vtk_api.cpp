@@ -280,16 +280,14 @@ int halo_exchange(vtk_csr *A, const double *x) {
     return comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble, sizeof(double));
 }
 
-// the same exchange overlapped: pack on the main stream, send/recv on the comm stream;
-// ev_halo marks the halo's arrival (the boundary tiles wait on it)
+// the same exchange overlapped: pack and send/recv both on the comm stream once x is final on
+// the main stream (ev_pack); the interior tiles start at once, ev_halo marks the halo's arrival
+// (the boundary tiles wait on it)
 int halo_exchange_async(vtk_csr *A, const double *x) {
     vtk_ctx *c = A->ctx;
-    {
-        Prof pf(c, "halo", -1, 16.0 * A->n_send);
-        HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
-    }
     HIPCHK(c, hipEventRecord(c->ev_pack, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_pack, 0));
+    HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->comm_stream));
     TRY(comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble,
                        sizeof(double), c->comm_stream));
     HIPCHK(c, hipEventRecord(c->ev_halo, c->comm_stream));
@@ -587,6 +585,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const double b_csr = (s.A->fp32 ? 8.0 : 12.0) * s.A->nnz + 4.0 * (n + 1);
     const double b_inv = bj_row_bytes(s.M) * n;
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
+    // (folding the finalize into the boundary launch's last workgroup was measured slower: one
+    // workgroup summing 2j+3 x ~1000 partials took as long as the 2j+3-workgroup launch)
     auto reduce_step = [&](int j, const double *w, int tag, int cnt) -> int {
         if (cnt == 0) {
             Prof pf(c, "dc_dots", tag, n8 * (j + (w ? 2 : 1)));
