@@ -1527,15 +1527,40 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
     const int with_w = closing ? 0 : 1;
     const int nq = with_w ? 2 * j + 3 : j + 1;
     const int M1 = m + 1;
-    // phase A: quantities, raw Hessenberg columns 0..j-1, rotations, S, scalars -> LDS
-    for (int b = wv; b < nq; b += nw) {
-        int qs;
-        if (b < j) qs = b;
-        else if (with_w && b < 2 * j) qs = DC_MAXJ + (b - j);
-        else qs = 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
-        const double acc = part ? wave_sum(strided_sum<GMAX / 64, 64>(part + (size_t)qs * GMAX, cnt, lane))
-                                : scal[qs];
-        if (lane == 0) q[qs] = acc;
+    // phase A: quantities, raw Hessenberg columns 0..j-1, rotations, S, scalars -> LDS.  A wave
+    // takes up to three quantities per round and issues all their partial loads before any add
+    // (one memory round trip for j <= 22 instead of one per quantity)
+    auto qslot = [&](int b) {
+        if (b < j) return b;
+        if (with_w && b < 2 * j) return DC_MAXJ + (b - j);
+        return 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
+    };
+    if (part) {
+        constexpr int PL = GMAX / 64;
+        for (int b0 = wv; b0 < nq; b0 += 3 * nw) {
+            double v[3][PL];
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const int b = b0 + h * nw;
+                const double *pp = part + (size_t)(b < nq ? qslot(b) : 0) * GMAX;
+#pragma unroll
+                for (int u = 0; u < PL; ++u) {
+                    const int i = lane + u * 64;
+                    v[h][u] = (b < nq && i < cnt) ? pp[i] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const int b = b0 + h * nw;
+                double acc = 0.0;
+#pragma unroll
+                for (int u = 0; u < PL; ++u) acc += v[h][u];
+                acc = wave_sum(acc);
+                if (b < nq && lane == 0) q[qslot(b)] = acc;
+            }
+        }
+    } else {
+        for (int b = tid; b < nq; b += blockDim.x) q[qslot(b)] = scal[qslot(b)];
     }
     for (int e = tid; e < j * (j + 1); e += blockDim.x) {
         const int i = e / (j + 1), k = e % (j + 1);
@@ -1558,12 +1583,17 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
     // column, S and the rotation go to global memory once
     auto rotate_commit = [&](int c, bool brk) -> bool {
         double *hc = hc_s;
+        // the running element stays in a register: only the loads of hc[k+1] and the rotation
+        // (independent of the chain) touch LDS
+        double cur = hc[0];
+#pragma unroll 4
         for (int k = 0; k < c; ++k) {
             const double cg = giv_s[2 * k], sg = giv_s[2 * k + 1];
-            const double n0 = hc[k], n1 = hc[k + 1];
-            hc[k] = cg * n0 + sg * n1;
-            hc[k + 1] = -sg * n0 + cg * n1;
+            const double n1 = hc[k + 1];
+            hc[k] = cg * cur + sg * n1;
+            cur = -sg * cur + cg * n1;
         }
+        hc[c] = cur;
         double cg, sg, mag;
         d_lartg(hc[c], hc[c + 1], cg, sg, mag);
         giv_s[2 * c] = cg;
@@ -1590,24 +1620,35 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
         }
         return false;
     };
-    // phase B (lane 0): r, finalise column j-1 (h += nu s, h_{j,j-1} = nu r) and rotate it
-    if (tid == 0) {
-        double ss = 0.0, sz = 0.0;
-        for (int k = 0; k < j; ++k) { ss += sv[k] * sv[k]; sz += sv[k] * zv[k]; }
+    // phase B1 (wave 0, lane k): r and column j-1 final (h += nu s, h_{j,j-1} = nu r) in parallel;
+    // the dots as butterfly sums (fixed tree, the same bits in every lane)
+    const bool fin_prev = j >= 1 && !flags[0];
+    if (wv == 0) {
+        const double svk = lane < j ? sv[lane] : 0.0, zvk = lane < j ? zv[lane] : 0.0;
+        const double ss = wave_allsum(svk * svk), sz = wave_allsum(svk * zvk);
         double r = 1.0;
         if (j >= 1) {
             const double r2 = alpha - ss;
             r = __builtin_sqrt(r2 > 0.0 ? r2 : alpha);
         }
-        sc[3] = r;
-        sc[4] = sz;
-        if (j >= 1 && !flags[0]) {
+        if (lane == 0) {
+            sc[3] = r;
+            sc[4] = sz;
+        }
+        if (fin_prev && lane <= j) {
             const int c = j - 1;
             double *hr = hr_s + c * (DC_MAXJ + 1);
-            const double nu = sc[1];
-            for (int k = 0; k < j; ++k) hr[k] = hr[k] + nu * sv[k];
-            hr[j] = nu * r;
-            for (int k = 0; k <= j; ++k) { Hraw[(size_t)c * M1 + k] = hr[k]; hc_s[k] = hr[k]; }
+            const double v = lane < j ? hr[lane] + sc[1] * sv[lane] : sc[1] * r;
+            hr[lane] = v;
+            Hraw[(size_t)c * M1 + lane] = v;
+            hc_s[lane] = v;
+        }
+    }
+    __syncthreads();
+    // phase B2 (lane 0): breakdown test, Givens and stop test of column j-1
+    if (tid == 0) {
+        if (fin_prev) {
+            const int c = j - 1;
             const bool brk = hc_s[j] <= DBL_EPSILON * sc[2];
             if (brk) hc_s[j] = 0.0;
             cf->committed[c] = 1;
@@ -1633,10 +1674,11 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
         if (k < j) cf->s[k] = sv[k];
     }
     __syncthreads();
-    if (tid != 0) return;
+    if (wv != 0) return;
+    const double ek = lane <= j ? e_s[lane] : 0.0;
+    const double ee = wave_allsum(ek * ek);
+    if (lane != 0) return;
     // phase D (lane 0): nu_{j+1}, update-pass scalars, early commit when unambiguous
-    double ee = 0.0;
-    for (int k = 0; k <= j; ++k) ee += e_s[k] * e_s[k];
     cf->rinv = 1.0 / r;
     const double gn = __builtin_sqrt(gamma) / r;
     const double nu2 = gamma - ee;
