@@ -1,0 +1,63 @@
+"""Edge cases of the device path: 1x1 and n < bs systems (padded BJ blocks), a partial last
+block under the tridiagonal BJ mode, n below one SELL chunk, an empty system, b = 0; every
+layout and BJ mode against the oracle."""
+import numpy as np
+import pytest
+
+from oracle import coracle, twin
+
+pytestmark = pytest.mark.gpu
+
+
+def tridiag(n, seed=1):
+    rng = np.random.default_rng(seed)
+    rows, cols, vals = [], [], []
+    for i in range(n):
+        for c in (i - 1, i, i + 1):
+            if 0 <= c < n:
+                rows.append(i)
+                cols.append(c)
+                vals.append(4.0 + rng.random() if c == i else -1.0 + 0.2 * rng.random())
+    ip = np.zeros(n + 1, np.int32)
+    np.add.at(ip, np.asarray(rows) + 1, 1)
+    return np.cumsum(ip).astype(np.int32), np.asarray(cols, np.int32), np.asarray(vals)
+
+
+@pytest.mark.parametrize("n,bs", [(1, 8), (5, 8), (7, 4), (63, 8), (65, 4), (130, 2)])
+@pytest.mark.parametrize("layout", ["sell", "csr"])
+@pytest.mark.parametrize("mode", ["inverse", "tridiag"])
+def test_small_systems(gpu, vk_lib, n, bs, layout, mode):
+    vk = vk_lib
+    ip, ix, d = tridiag(n)
+    A = vk.csr_matrix((d, ix, ip), shape=(n, n), ctx=gpu)
+    A.set_layout(layout)
+    x = twin.rhs(n, seed=0xC0FFEE)
+    assert np.array_equal(A @ x, coracle.spmv(ip, ix, d, x))
+    M = vk.block_jacobi(A, bs, mode=mode)
+    assert M.mode == mode
+    inv = coracle.bj_setup(ip, ix, d, bs)
+    assert np.array_equal(M.inverse(), inv)
+    b = twin.rhs(n)
+    z = M @ b
+    ref_z = coracle.bj_apply(inv, b)
+    if mode == "inverse":
+        assert np.array_equal(z, ref_z)
+    else:
+        np.testing.assert_allclose(z, ref_z, rtol=1e-12, atol=1e-14 * np.abs(ref_z).max())
+    ref = coracle.gmres(ip, ix, d, b, inv, rtol=1e-10)
+    xs, info = vk.gmres(A, b, rtol=1e-10, M=M)
+    assert info == ref.info == 0
+    assert abs(vk.last_stats().inner_iters - ref.inner_iters) <= 1
+    np.testing.assert_allclose(xs, ref.x, rtol=1e-8, atol=1e-12)
+
+
+def test_zero_rhs_and_empty(gpu, vk_lib):
+    vk = vk_lib
+    ip, ix, d = tridiag(100)
+    A = vk.csr_matrix((d, ix, ip), shape=(100, 100), ctx=gpu)
+    x, info = vk.gmres(A, np.zeros(100), M=vk.block_jacobi(A, 4))
+    assert info == 0 and not x.any()                       # iterative.py: b = 0 -> x = 0
+    E = vk.csr_matrix((np.zeros(0), np.zeros(0, np.int32), np.zeros(1, np.int32)), shape=(0, 0), ctx=gpu)
+    assert (E @ np.zeros(0)).shape == (0,)
+    with pytest.raises(ValueError):
+        vk.gmres(E, np.zeros(0))
