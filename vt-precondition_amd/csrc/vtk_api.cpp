@@ -135,10 +135,11 @@ BjOp bj_op(const vtk_prec *M) {
     return o;
 }
 
-// algorithmic bytes per row of one BJ application
+// algorithmic bytes per row of one BJ application (tridiagonal: the SELL kernels read only m)
 double bj_row_bytes(const vtk_prec *M) {
     if (!M) return 0.0;
-    return bj_op(M).tri ? 24.0 : 8.0 * M->bs;
+    if (bj_op(M).tri) return M->A->use_sell ? 8.0 : 24.0;
+    return 8.0 * M->bs;
 }
 
 // reducing-kernel grid: a function of the local size on one GPU; GMAX on every rank when

@@ -167,6 +167,39 @@ __device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, 
     return A;
 }
 
+// The same solve from m alone (SELL kernels): the lane has its row's block sub/super-diagonal
+// entries from the SpMV loop (duplicates summed in stored order, as in the setup), so
+// l_i = sub_i m_{i-1} (m_{i-1} from the neighbour lane) and g_i = sup_i m_i: 8 B per row.
+template <int BS>
+__device__ __forceinline__ double bj_trim_group(double y, bool act, int64_t row, int lane, double sub, double sup,
+                                                const double *m_arr) {
+    const int ii = lane & (BS - 1);
+    const double m = act ? m_arr[row] : 1.0;
+    const double mprev = __shfl_up(m, 1, BS);
+    const double l = ii > 0 ? sub * mprev : 0.0;
+    const double g = sup * m;
+    double A = y, B = -l;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double Ap = __shfl_up(A, off, BS), Bp = __shfl_up(B, off, BS);
+        if (ii >= off) {
+            A = A + B * Ap;
+            B = B * Bp;
+        }
+    }
+    A = m * A;
+    B = -g;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double An = __shfl_down(A, off, BS), Bn = __shfl_down(B, off, BS);
+        if (ii + off < BS) {
+            A = A + B * An;
+            B = B * Bn;
+        }
+    }
+    return A;
+}
+
 // Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
 // 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
 // contiguous id range; with the grid-stride tile loop an XCD then works on a contiguous window
@@ -244,9 +277,10 @@ __device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, dou
 // Epilogue of one row (both layouts): y[row] from the row sum s, per-lane partial sums.  All
 // lanes of the wave call it (the BJ groups exchange values by shuffles); act = a real row.
 // Returns the value written (w for the DCGS2 dots).
-template <typename VT, bool HALO, int EPI, int BS, bool TRI>
+// TRIM: the tridiagonal solve from m and the row's sub/sup (SELL); else from l | m | g.
+template <typename VT, bool HALO, int EPI, int BS, bool TRI, bool TRIM = false>
 __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double s, int row, bool act, int lane,
-                                               double &acc0, double &acc1) {
+                                               double &acc0, double &acc1, double sub = 0.0, double sup = 0.0) {
     constexpr bool DC = EPI == EPI_PREC_DC;
     if constexpr (EPI == EPI_PLAIN) {
         if (act) a.y[row] = s;
@@ -266,7 +300,9 @@ __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double 
             acc0 += sv * sv;
         }
         double z = sv;
-        if constexpr (BS > 0 && TRI) {
+        if constexpr (BS > 0 && TRI && TRIM) {
+            z = bj_trim_group<BS>(sv, act, row, lane, sub, sup, a.tri + a.tri_ld);
+        } else if constexpr (BS > 0 && TRI) {
             z = bj_tri_group<BS>(sv, act, row, lane, a.tri, a.tri_ld);
         } else if constexpr (BS > 0) {
             // z_i = sum_j inv[i][j] * y_j over the BS lanes of this block
@@ -436,9 +472,9 @@ __device__ __forceinline__ double wave_allsum(double v) {
 
 template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_sell(SpmvK<VT, HALO> a) {
-    constexpr int SW = 8;   // entries per load batch
+    constexpr int SW = EPI == EPI_PREC_DC ? 6 : 8;   // entries per load batch (DC: registers)
     constexpr int KB = 4;   // basis vectors per load batch (DC)
-    constexpr int JB = 12;  // basis vectors with per-lane register accumulators (DC)
+    constexpr int JB = 10;  // basis vectors with per-lane register accumulators (DC)
     constexpr bool DC = EPI == EPI_PREC_DC;
     constexpr int NQW = 2 * DC_MAXJ + 3;      // per-wave partial record (DC)
     __shared__ double stage[(NT / 64) * NQW];
@@ -458,6 +494,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const int row = 64 * q + lane;
         const bool act = row < a.n_local;
         double s = 0.0;
+        double sub = 0.0, sup = 0.0;   // TRI: the row's block sub/super-diagonal entries
+        constexpr bool TRIM = TRI && BS > 0;
+        [[maybe_unused]] const int ii = lane & (BS > 0 ? BS - 1 : 0);
         if (64 * q < a.n_local) {
             const int64_t o0 = a.sell_off[q];
             const int w = (int)((a.sell_off[q + 1] - o0) >> 6);
@@ -478,9 +517,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
                 for (int u = 0; u < SW; ++u)
                     if (c[u] >= 0) s += d[u] * xv[u];
+                if constexpr (TRIM) {
+#pragma unroll
+                    for (int u = 0; u < SW; ++u) {
+                        if (c[u] == row - 1 && ii > 0) sub = sub + d[u];
+                        if (c[u] == row + 1 && ii < BS - 1) sup = sup + d[u];
+                    }
+                }
             }
         }
-        const double z = row_epilogue<VT, HALO, EPI, BS, TRI>(a, s, row, act, lane, acc0, acc1);
+        const double z = row_epilogue<VT, HALO, EPI, BS, TRI, TRIM>(a, s, row, act, lane, acc0, acc1, sub, sup);
         if constexpr (DC) {
             const double pv = act ? a.x[row] : 0.0;   // p_j (= the SpMV input) on this row
             daa += pv * pv;
