@@ -458,11 +458,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // bit-identical).
 //
 // DCGS2 dots (EPI_PREC_DC), wave-local: each lane already holds its row's w and p, so the wave
-// reads V[k][row] for every k < j itself (8 loads in flight per batch, no LDS staging, no
-// barrier).  The first DC_JB vectors accumulate per lane in registers and are reduced once at
-// the end; vectors beyond (j > 16) are reduced per chunk with a butterfly (every lane gets the
-// same bits) and lane k keeps their running sums.  C3: the LDS-staged split of the vectors
-// over the waves cost 462 us + 33.4 us per vector, butterflies for every vector 320 us + 68 us.
+// reads V[k][row] for every k < j itself (4 loads in flight per batch, no LDS staging, no
+// barrier).  The first JB = 10 vectors accumulate per lane in registers and are reduced once
+// at the end; vectors beyond are reduced per chunk with a butterfly (every lane gets the same
+// bits) and lane k keeps their running sums.  C3: the LDS-staged split of the vectors over the
+// waves cost 462 us + 33.4 us per vector, butterflies for every vector 320 us + 68 us, this
+// ~360 us + 29 us per register vector.  Tried and measured slower on one box (A/B): 20
+// register vectors at 3 waves/SIMD (-2 %), k >= 10 handed to k_dc_dots (-3 %).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ double wave_allsum(double v) {
 #pragma unroll
@@ -539,11 +541,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 double v[KB];
 #pragma unroll
                 for (int u = 0; u < KB; ++u)
-                    v[u] = (k0 + u < a.j && act) ? __builtin_nontemporal_load(vb + (size_t)(k0 + u) * a.ld) : 0.0;
+                    v[u] = (k0 + u < JB && k0 + u < a.j && act)
+                               ? __builtin_nontemporal_load(vb + (size_t)(k0 + u) * a.ld) : 0.0;
 #pragma unroll
                 for (int u = 0; u < KB; ++u) {
-                    as_[k0 + u] += v[u] * pv;
-                    az_[k0 + u] += v[u] * z;
+                    if (k0 + u < JB) {   // compile-time after unrolling: JB need not divide by KB
+                        as_[k0 + u] += v[u] * pv;
+                        az_[k0 + u] += v[u] * z;
+                    }
                 }
             }
             for (int k0 = JB; k0 < a.j; k0 += KB) {

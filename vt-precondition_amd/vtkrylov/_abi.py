@@ -117,9 +117,10 @@ def lib() -> C.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"libvtkrylov.so not built: {LIB_PATH} (run __graft_entry__.build())")
-        L = C.CDLL(LIB_PATH)
+        path = os.environ.get("VTK_LIB", LIB_PATH)   # VTK_LIB: another build of the same ABI (A/B runs)
+        if not os.path.exists(path):
+            raise ImportError(f"libvtkrylov.so not built: {path} (run __graft_entry__.build())")
+        L = C.CDLL(path)
         for name, (res, args) in PROTOTYPES.items():
             f = getattr(L, name)
             f.restype = res
