@@ -149,3 +149,14 @@ def test_library_is_current():
         [os.path.join(root, "include", "vtkrylov.h")]
     stale = [s for s in srcs if os.path.getmtime(s) > os.path.getmtime(so)]
     assert not stale, f"libvtkrylov.so is older than {stale}"
+
+
+@pytest.mark.slow
+def test_host_code_under_asan_ubsan():
+    """tools/asan_host.sh: the host routines under AddressSanitizer + UBSan (CPU only)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(root, "tools", "asan_host.sh")], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and "asan_host: ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
