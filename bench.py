@@ -113,8 +113,9 @@ def main():
     ap.add_argument("--bj-mode", default="auto", choices=["auto", "inverse", "tridiag"],
                     help="block-Jacobi apply: auto (tridiagonal-block LU factors when every block is "
                          "tridiagonal, as on the Vlasov operators), inverse (bit-exact inv*r), tridiag")
-    ap.add_argument("--layout", default="auto", choices=["auto", "sell", "csr"],
-                    help="SpMV layout: auto (SELL-64 when its padding is small), sell, csr (CSR-stream tiles)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "sell", "sell32", "csr"],
+                    help="SpMV layout: auto (SELL-64 when its padding is small), sell (dictionary-coded "
+                         "columns), sell32 (int32 columns), csr (CSR-stream tiles)")
     ap.add_argument("--comm-solo", action="store_true",
                     help="one GPU through the distributed code paths (one-rank RCCL communicator)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -215,7 +216,11 @@ def main():
     ev1.record(stream)
     ev1.synchronize()
     t_spmv = ev0.elapsed_time(ev1) / 1e3 / args.spmv_reps
-    B = spmv_bytes(A.nnz, A.n_local, fp32)
+    # bytes the SpMV reads/writes in the layout in use (dictionary-coded SELL columns are
+    # 0.5 B + 1 B/row instead of 4 B per entry); csr_equiv: SURVEY §8d's CSR figure
+    linfo = A.layout_info()
+    B = linfo["matrix_bytes"] + 16 * A.n_local
+    B_csr = spmv_bytes(A.nnz, A.n_local, fp32)
     spmv_gbs = B / t_spmv / 1e9
     # cold: median of single reps with the 256 MB Infinity Cache flushed in between
     flush = torch.empty(512 * 2**20 // 8, dtype=torch.float64, device=dev)
@@ -287,6 +292,8 @@ def main():
         "info": infos,
         "true_rel_residual": rel_res,
         "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B,
+                 "layout": linfo["layout"], "wide_chunks": linfo["wide_chunks"],
+                 "csr_equiv_bytes": B_csr, "csr_equiv_gbs": B_csr / t_spmv / 1e9,
                  "cold_median_us": t_cold * 1e6, "cold_gbs": B / t_cold / 1e9,
                  "device_copy_gbs": copy_gbs, "frac_of_copy": spmv_gbs / copy_gbs,
                  "device_read_gbs": read_gbs, "frac_of_read": spmv_gbs / read_gbs},
@@ -295,7 +302,7 @@ def main():
                      "traffic": traffic, "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],
                      "avg_us": dk["avg_us"], "launches": dk["launches"],
                      "share_of_solve": dk["seconds"] / tot_s},
-        "roofline_spmv": {"kernel": "spmv (plain CSR-stream, vtk_spmv)", "bound": "hbm",
+        "roofline_spmv": {"kernel": f"spmv ({linfo['layout']}, vtk_spmv)", "bound": "hbm",
                           "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": spmv_gbs / HBM_PEAK_GBS, "traffic": pmc_traffic("spmv", args.config, world),
                           "algorithmic_bytes_per_launch": B},

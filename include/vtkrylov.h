@@ -75,8 +75,19 @@ typedef enum {
 typedef enum {
     VTK_LAYOUT_AUTO = 0, /* default: SELL when its padding is <= 25 % of nnz, else CSR        */
     VTK_LAYOUT_CSR = 1,  /* CSR-stream tiles (products staged in LDS, one lane per row)       */
-    VTK_LAYOUT_SELL = 2  /* SELL-64 copy: one wavefront per 64 rows, entries column-major     */
+    VTK_LAYOUT_SELL = 2, /* SELL-64 copy: one wavefront per 64 rows, entries column-major;
+                          * columns dictionary-coded per 64-row chunk (4-bit codes into the
+                          * chunk's <= 15 distinct col-row offsets; chunks with more keep int32) */
+    VTK_LAYOUT_SELL32 = 3 /* SELL-64 with int32 columns everywhere                              */
 } vtk_layout;
+
+/* what vtk_csr_layout_info reports: the layout in use and the bytes one SpMV reads of the
+ * operator in it (values, columns or codes + dictionaries, offsets)                          */
+typedef struct {
+    int layout;              /* vtk_layout in use (never AUTO)                                */
+    double matrix_bytes;
+    int64_t sell_chunks, sell_entries, wide_chunks;
+} vtk_layout_info;
 
 /* Synthetic Vlasov operator parameters. */
 typedef struct {
@@ -169,6 +180,7 @@ void vtk_csr_destroy(vtk_csr *A);
  * 12 B per padded entry, 8 B with f32 values) */
 int vtk_csr_set_layout(vtk_csr *A, int layout);
 int vtk_csr_get_layout(vtk_csr *A, int *layout_in_use);
+int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out);
 
 /* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged
  * internally over RCCL when world > 1).  Bit-identical to csr_matvec (serial row sums). */

@@ -35,6 +35,8 @@ for s in "$@"; do
         gridscan) for G in 512 768 896 960 1000 1024; do VTK_SELL_GRID=$G step grid$G 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; done ;;
         profmgs) step profmgs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profmgs -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --orth mgs ;;
         ab) for v in a cur a cur; do if [ $v = a ]; then L=tools/bin/lib_a/libvtkrylov.so; else L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; fi; VTK_LIB=$L step ab_$v 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; grep -o '"value": [0-9.]*' gpurun_out/ab_$v.log; done ;;
+        variants) for rep in 1 2; do for v in cur ${VARIANTS:-a}; do if [ $v = cur ]; then L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; else L=tools/bin/lib_$v/libvtkrylov.so; fi; VTK_LIB=$L step var_${v}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 ${BENCH_ARGS:-} || exit $?; python tools/bench_brief.py gpurun_out/var_${v}_$rep.log; done; done ;;
+        abargs) IFS=';' read -ra AL <<< "${ABARGS:-}"; for rep in 1 2; do i=0; for ar in "${AL[@]}"; do i=$((i+1)); step abargs_${i}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 $ar || exit $?; echo "[$ar]"; python tools/bench_brief.py gpurun_out/abargs_${i}_$rep.log; done; done ;;
         benchmgs) step benchmgs 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth mgs ;;
         benchdc) step benchdc 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --orth dcgs2 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;

@@ -24,7 +24,7 @@ def tridiag(n, seed=1):
 
 
 @pytest.mark.parametrize("n,bs", [(1, 8), (5, 8), (7, 4), (63, 8), (65, 4), (130, 2)])
-@pytest.mark.parametrize("layout", ["sell", "csr"])
+@pytest.mark.parametrize("layout", ["sell", "sell32", "csr"])
 @pytest.mark.parametrize("mode", ["inverse", "tridiag"])
 def test_small_systems(gpu, vk_lib, n, bs, layout, mode):
     vk = vk_lib

@@ -73,7 +73,7 @@ def test_device_generator_hash_c4(gpu, vk_lib, golden_large):
     assert hashlib.sha256(d.tobytes()).hexdigest() == ref["data"]
 
 
-@pytest.mark.parametrize("layout", ["sell", "csr"])
+@pytest.mark.parametrize("layout", ["sell", "sell32", "csr"])
 @pytest.mark.parametrize("name", SMALL + ["C1"])
 def test_spmv_bitexact(ops, golden, name, layout):
     p, A, (ip, ix, d) = ops[name]
@@ -105,14 +105,62 @@ def test_spmv_ragged_sell_forced_bitexact(gpu, vk_lib, golden):
     n = ip.shape[0] - 1
     A = vk.csr_matrix((d, ix, ip), shape=(n, n), ctx=gpu)
     assert A.layout == "csr"            # auto: padding too large for SELL
-    A.set_layout("sell")
-    assert A.layout == "sell"
     x = twin.rhs(n, seed=0xC0FFEE)
-    assert np.array_equal(A @ x, coracle.spmv(ip, ix, d, x))
-    assert np.array_equal(A @ x, golden["ragged/spmv_y"])
+    for lay in ("sell", "sell32"):
+        A.set_layout(lay)
+        assert A.layout == lay
+        assert np.array_equal(A @ x, coracle.spmv(ip, ix, d, x))
+        assert np.array_equal(A @ x, golden["ragged/spmv_y"])
+    A.set_layout("sell")
+    assert A.layout_info()["wide_chunks"] > 0     # random columns: int32 chunks
 
 
-@pytest.mark.parametrize("layout", ["sell", "csr"])
+def _dict_edge_csr():
+    """Chunk 0: exactly 15 distinct col-row offsets (coded); chunk 1: 16 (int32, "wide");
+    chunk 2: ragged rows over 3 offsets incl. empty rows and unsorted duplicates; chunk 3:
+    empty; chunk 4: 40-entry rows (5 code words per lane) over 2 offsets."""
+    n = 320
+    rows, cols = [], []
+    for r in range(64):
+        for o in range(15):
+            rows.append(r); cols.append(r + 3 * o)
+    for r in range(64, 128):
+        for o in range(16):
+            rows.append(r); cols.append(r + 2 * o - 10)
+    rng = np.random.default_rng(7)
+    for r in range(128, 192):
+        for _ in range(int(rng.integers(0, 6))):
+            rows.append(r); cols.append(r + int(rng.choice([-5, 0, 9])))
+    for r in range(256, 320):
+        for k in range(40):
+            rows.append(r); cols.append(r - 1 if k % 2 else r - 200)
+    rows, cols = np.array(rows), np.array(cols)
+    vals = np.random.default_rng(8).standard_normal(rows.size)
+    order = np.argsort(rows, kind="stable")
+    rows, cols, vals = rows[order], cols[order], vals[order]
+    ip = np.zeros(n + 1, np.int32)
+    np.add.at(ip, rows + 1, 1)
+    return n, np.cumsum(ip).astype(np.int32), cols.astype(np.int32), vals
+
+
+def test_spmv_dictionary_chunks_bitexact(gpu, vk_lib):
+    """SELL column dictionaries: the 15-offset limit, a wide chunk next to coded ones, ragged
+    and empty rows, long rows spanning several code words -- bit-identical to csr_matvec."""
+    vk = vk_lib
+    n, ip, ix, d = _dict_edge_csr()
+    A = vk.csr_matrix((d, ix, ip), shape=(n, n), ctx=gpu)
+    x = twin.rhs(n, seed=0xC0FFEE)
+    ref = coracle.spmv(ip, ix, d, x)
+    for lay in ("sell", "sell32", "csr"):
+        A.set_layout(lay)
+        assert A.layout == lay
+        assert np.array_equal(A @ x, ref), lay
+    A.set_layout("sell")
+    li = A.layout_info()
+    assert li["sell_chunks"] == 5 and li["wide_chunks"] == 1
+
+
+@pytest.mark.parametrize("layout", ["sell", "sell32", "csr"])
 @pytest.mark.parametrize("bj_mode", ["tridiag", "inverse"])
 def test_gmres_layouts_c1(ops, layout, bj_mode):
     p, A, (ip, ix, d) = ops["C1"]

@@ -384,12 +384,37 @@ int setup_halo(vtk_csr *A) {
     return VTK_OK;
 }
 
+void free_pack(vtk_csr *A) {
+    (void)hipFree(A->sell.d_pk);
+    (void)hipFree(A->sell.d_pkoff);
+    (void)hipFree(A->sell.d_dict);
+    A->sell.d_pk = nullptr;
+    A->sell.d_pkoff = nullptr;
+    A->sell.d_dict = nullptr;
+    A->sell.n_wide = 0;
+}
+
 void free_sell(vtk_csr *A) {
+    free_pack(A);
     (void)hipFree(A->sell.d_off);
     (void)hipFree(A->sell.d_col);
     (void)hipFree(A->sell.d_val);
     A->sell = Sell{};
     A->use_sell = false;
+}
+
+// Bytes of the operator one SpMV reads in the layout in use (the algorithmic figure of the
+// profile classes): CSR = values + int32 columns + indptr; SELL = values
+// (padding included) + offsets, + int32 columns, or (dictionary-coded) 4-bit codes + 64-B
+// dictionaries + the wide chunks' int32 columns.
+double matrix_bytes(const vtk_csr *A) {
+    const double vb = A->fp32 ? 4.0 : 8.0;
+    if (!A->use_sell) return (vb + 4.0) * A->nnz + 4.0 * (A->n_local + 1);
+    const Sell &sl = A->sell;
+    double b = vb * sl.entries + 8.0 * (sl.nch + 1);
+    if (sl.d_pk) b += 4.0 * sl.pk_words + 72.0 * sl.nch + 4.0 * sl.wide_entries;
+    else b += 4.0 * sl.entries;
+    return b;
 }
 
 // SELL-64 copy of the (local-index) CSR on the device.  only_if_compact: stop after the
@@ -424,6 +449,40 @@ int build_sell(vtk_csr *A, bool only_if_compact, bool *built) {
     sl.nch = nch;
     A->sell = sl;
     *built = true;
+    return VTK_OK;
+}
+
+// Dictionary-coded columns of the SELL copy (k_sell_pack); the int32 columns stay for the
+// chunks with too many distinct offsets.  Best effort: out of memory leaves the copy unpacked.
+int build_pack(vtk_csr *A) {
+    vtk_ctx *c = A->ctx;
+    Sell &sl = A->sell;
+    if (sl.d_pk || !sl.d_col) return VTK_OK;
+    const int64_t nch = sl.nch;
+    const size_t scan_bytes = std::max<size_t>(sell_scan_bytes(A->n_local), 16);
+    DBuf tmp, scan, cnt;
+    TRY(dalloc(c, tmp, (size_t)(nch + 1) * sizeof(int64_t)));
+    TRY(dalloc(c, scan, scan_bytes));
+    TRY(dalloc(c, cnt, 2 * sizeof(unsigned long long)));
+    int64_t words = 0;
+    unsigned long long wide[2] = {0, 0};
+    hipError_t e = hipMalloc(&sl.d_pkoff, (size_t)(nch + 1) * sizeof(int64_t));
+    if (e == hipSuccess) e = launch_sell_pack(sl.d_off, nch, sl.d_pkoff, tmp.as<int64_t>(), scan.p, scan_bytes, nullptr,
+                                              nullptr, nullptr, nullptr, 0, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&words, sl.d_pkoff + nch, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMalloc(&sl.d_pk, (size_t)std::max<int64_t>(words, 1) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&sl.d_dict, (size_t)std::max<int64_t>(nch, 1) * 16 * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(cnt.p, 0, 2 * sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess) e = launch_sell_pack(sl.d_off, nch, sl.d_pkoff, nullptr, nullptr, 0, sl.d_col, sl.d_pk,
+                                              sl.d_dict, cnt.as<unsigned long long>(), 1, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(wide, cnt.p, sizeof(wide), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); free_pack(A); return VTK_OK; }
+    if (e != hipSuccess) { free_pack(A); return fail(c, VTK_ERR_HIP, std::string("SELL pack: ") + hipGetErrorString(e)); }
+    sl.n_wide = (int64_t)wide[0];
+    sl.wide_entries = (int64_t)wide[1];
+    sl.pk_words = words;
     return VTK_OK;
 }
 
@@ -469,6 +528,8 @@ int apply_layout(vtk_csr *A, int layout) {
         TRY(build_sell(A, layout == VTK_LAYOUT_AUTO, &built));
         A->use_sell = built;
         if (built && !A->g_all.grid) TRY(build_groups(A));
+        if (built && layout == VTK_LAYOUT_SELL32) free_pack(A);
+        else if (built) TRY(build_pack(A));
     }
     A->layout = layout;
     (void)c;
@@ -539,7 +600,7 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
     TRY(halo_exchange(A, v));
     const double *v0 = want_dots ? s.V : nullptr;
     const double n8 = 8.0 * s.n;
-    const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (s.n + 1);
+    const double b_csr = matrix_bytes(A);
     const double b_inv = bj_row_bytes(s.M) * s.n;
     int cnt;
     if (!s.M) {
@@ -583,7 +644,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // would spill the fused kernel's registers)
     const bool fused = bj_fused(s.M) && s.M->bs <= 8;
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
-    const double b_csr = (s.A->fp32 ? 8.0 : 12.0) * s.A->nnz + 4.0 * (n + 1);
+    const double b_csr = matrix_bytes(s.A);
     const double b_inv = bj_row_bytes(s.M) * n;
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
     // (folding the finalize into the boundary launch's last workgroup was measured slower: one
@@ -703,7 +764,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(GmresState), hipMemcpyHostToDevice, c->stream));
     int rc;
     const double n8 = 8.0 * n;
-    const double b_spmv = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 2 * n8;
+    const double b_spmv = matrix_bytes(A) + 2 * n8;
     const double b_pc = bj_row_bytes(M) * n + 2 * n8;
     // ||b|| and ||M b|| (iterative.py:708, :714)
     { Prof pf(c, "dot", -1, n8);
@@ -723,7 +784,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const Tiles *rtiles = (M && bj_fused(M)) ? &M->tiles : &A->tiles;
     const SpmvIn rin0 = spmv_in(A, rtiles, x), pin0 = spmv_in(A, &A->tiles, x);
     double *prr = c->d_part + 4 * GMAX, *prz = c->d_part + 5 * GMAX;
-    const double b_csr = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1);
+    const double b_csr = matrix_bytes(A);
     Red rz{prz, spmv_grid(rin0)};
     auto residual = [&]() -> int {
         TRY(halo_exchange(A, x));
@@ -772,7 +833,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     double ptol_max_factor = 1.0;
     double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);   // :723
     double presid = 0.0;
-    const double bytes_spmv = (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 16.0 * n;
+    const double bytes_spmv = matrix_bytes(A) + 16.0 * n;
     const double bytes_pc = M ? (8.0 * M->bs * n + 16.0 * n) : 16.0 * n;
     hipEvent_t ev[LOOKAHEAD + 1];
     for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1132,7 +1193,7 @@ int vtk_spmv(vtk_csr *A, const double *x, double *y, int kind) {
     TRY(stage_in(c, kind == VTK_PTR_DEVICE ? y : nullptr, A->n_local, kind, sy));
     TRY(halo_exchange(A, sx.d));
     {
-        Prof pf(c, "spmv", -1, (A->fp32 ? 8.0 : 12.0) * A->nnz + 4.0 * (A->n_local + 1) + 16.0 * A->n_local);
+        Prof pf(c, "spmv", -1, matrix_bytes(A) + 16.0 * A->n_local);
         HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, sx.d), EPI_PLAIN, sy.d, nullptr, BjOp{}, nullptr, nullptr, nullptr, nullptr, 0, c->stream));
     }
     if (c->prof_on) prof_flush(c);
@@ -1230,7 +1291,8 @@ int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
 int vtk_csr_set_layout(vtk_csr *A, int layout) {
     if (!A) return VTK_ERR_ARG;
     vtk_ctx *c = A->ctx;
-    if (layout != VTK_LAYOUT_AUTO && layout != VTK_LAYOUT_CSR && layout != VTK_LAYOUT_SELL)
+    if (layout != VTK_LAYOUT_AUTO && layout != VTK_LAYOUT_CSR && layout != VTK_LAYOUT_SELL &&
+        layout != VTK_LAYOUT_SELL32)
         return fail(c, VTK_ERR_ARG, "vtk_csr_set_layout: unknown layout");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1239,7 +1301,21 @@ int vtk_csr_set_layout(vtk_csr *A, int layout) {
 
 int vtk_csr_get_layout(vtk_csr *A, int *layout_in_use) {
     if (!A || !layout_in_use) return VTK_ERR_ARG;
-    *layout_in_use = A->use_sell ? VTK_LAYOUT_SELL : VTK_LAYOUT_CSR;
+    *layout_in_use = A->use_sell ? (A->sell.d_pk ? VTK_LAYOUT_SELL : VTK_LAYOUT_SELL32) : VTK_LAYOUT_CSR;
+    return VTK_OK;
+}
+
+int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out) {
+    if (!A || !out) return VTK_ERR_ARG;
+    vtk_layout_info li{};
+    int lay = VTK_LAYOUT_CSR;
+    (void)vtk_csr_get_layout(A, &lay);
+    li.layout = lay;
+    li.matrix_bytes = matrix_bytes(A);
+    li.sell_chunks = A->use_sell ? A->sell.nch : 0;
+    li.sell_entries = A->use_sell ? A->sell.entries : 0;
+    li.wide_chunks = A->use_sell && A->sell.d_pk ? A->sell.n_wide : 0;
+    *out = li;
     return VTK_OK;
 }
 

@@ -70,7 +70,18 @@ struct Sell {
     int32_t *d_col = nullptr;   // [entries], -1 = padding
     void *d_val = nullptr;      // [entries] f64 (C4: f32)
     int64_t nch = 0, entries = 0;
+    // dictionary-coded columns (k_sell_pack): entry k of row 64q+l is the 4-bit code
+    // (pk[pk_off[q] + 64*(k/8) + l] >> 4*(k%8)) & 15; code 15 = padding, else
+    // col = row + dict[16q + code].  dict[16q + 15] != 0: the chunk has more than
+    // PK_CODES distinct (col - row) offsets and reads d_col instead ("wide")
+    uint32_t *d_pk = nullptr;
+    int64_t *d_pkoff = nullptr;  // [nch+1] word offsets (multiples of 64)
+    int32_t *d_dict = nullptr;   // [nch][16]
+    int64_t n_wide = 0;          // chunks that kept int32 columns
+    int64_t wide_entries = 0;    // their entries (64 per row slot)
+    int64_t pk_words = 0;
 };
+constexpr int PK_CODES = 15;     // offsets per chunk dictionary (codes 0..14; 15 = padding)
 
 // groups of 4 SELL chunks (256 rows) a SELL launch covers: all (d_list null) or a list
 struct Groups {
@@ -205,6 +216,11 @@ hipError_t launch_sell_build(const int32_t *indptr, const int32_t *indices, cons
                              int64_t *off, int64_t *tmp64, void *scan_tmp, size_t scan_bytes, int32_t *col,
                              void *val, int phase, hipStream_t s);
 size_t sell_scan_bytes(int64_t n);
+// dictionary-coded columns of a built SELL: phase 0 = word offsets + scan into pkoff (tmp64
+// [nch+1], scan_tmp as above), phase 1 = codes + dictionaries, n_wide counted into *wide_cnt
+hipError_t launch_sell_pack(const int64_t *off, int64_t nch, int64_t *pkoff, int64_t *tmp64, void *scan_tmp,
+                            size_t scan_bytes, const int32_t *col, uint32_t *pk, int32_t *dict,
+                            unsigned long long *wide_cnt, int phase, hipStream_t s);
 hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
                                int64_t n, int bs, const double *inv, double *tri, int64_t ld, int *flags,
                                hipStream_t s);

@@ -108,6 +108,10 @@ struct SpmvK {
     const VT *sell_val;
     const int32_t *group_list;
     int ngroups;
+    // dictionary-coded columns (Sell::d_pk; null: int32 columns everywhere)
+    const uint32_t *pk;
+    const int64_t *pk_off;
+    const int32_t *dict;
 };
 
 template <typename VT, bool HALO>
@@ -171,10 +175,8 @@ __device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, 
 // entries from the SpMV loop (duplicates summed in stored order, as in the setup), so
 // l_i = sub_i m_{i-1} (m_{i-1} from the neighbour lane) and g_i = sup_i m_i: 8 B per row.
 template <int BS>
-__device__ __forceinline__ double bj_trim_group(double y, bool act, int64_t row, int lane, double sub, double sup,
-                                                const double *m_arr) {
+__device__ __forceinline__ double bj_trim_group(double y, int lane, double sub, double sup, double m) {
     const int ii = lane & (BS - 1);
-    const double m = act ? m_arr[row] : 1.0;
     const double mprev = __shfl_up(m, 1, BS);
     const double l = ii > 0 ? sub * mprev : 0.0;
     const double g = sup * m;
@@ -280,7 +282,8 @@ __device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, dou
 // TRIM: the tridiagonal solve from m and the row's sub/sup (SELL); else from l | m | g.
 template <typename VT, bool HALO, int EPI, int BS, bool TRI, bool TRIM = false>
 __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double s, int row, bool act, int lane,
-                                               double &acc0, double &acc1, double sub = 0.0, double sup = 0.0) {
+                                               double &acc0, double &acc1, double sub = 0.0, double sup = 0.0,
+                                               bool have_m = false, double mrow = 1.0, bool store = true) {
     constexpr bool DC = EPI == EPI_PREC_DC;
     if constexpr (EPI == EPI_PLAIN) {
         if (act) a.y[row] = s;
@@ -301,7 +304,8 @@ __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double 
         }
         double z = sv;
         if constexpr (BS > 0 && TRI && TRIM) {
-            z = bj_trim_group<BS>(sv, act, row, lane, sub, sup, a.tri + a.tri_ld);
+            if (!have_m) mrow = act ? a.tri[a.tri_ld + row] : 1.0;
+            z = bj_trim_group<BS>(sv, lane, sub, sup, mrow);
         } else if constexpr (BS > 0 && TRI) {
             z = bj_tri_group<BS>(sv, act, row, lane, a.tri, a.tri_ld);
         } else if constexpr (BS > 0) {
@@ -317,7 +321,7 @@ __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double 
             }
         }
         if (act) {
-            a.y[row] = z;
+            if (store) a.y[row] = z;
             if constexpr (EPI == EPI_RESID_PREC) {
                 acc1 += z * z;
             } else if constexpr (!DC) {
@@ -472,12 +476,29 @@ __device__ __forceinline__ double wave_allsum(double v) {
     return v;
 }
 
+#ifndef VTK_DC_KB
+#define VTK_DC_KB 4
+#endif
+#ifndef VTK_DC_JB
+#define VTK_DC_JB 10
+#endif
+#ifndef VTK_DC_PSW
+#define VTK_DC_PSW 4
+#endif
+#ifndef VTK_DC_HOIST
+#define VTK_DC_HOIST 1
+#endif
+#ifndef VTK_DC_WLATE
+#define VTK_DC_WLATE 0
+#endif
 template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_sell(SpmvK<VT, HALO> a) {
-    constexpr int SW = EPI == EPI_PREC_DC ? 6 : 8;   // entries per load batch (DC: registers)
-    constexpr int KB = 4;   // basis vectors per load batch (DC)
-    constexpr int JB = 10;  // basis vectors with per-lane register accumulators (DC)
+    constexpr int PSW = EPI == EPI_PREC_DC ? VTK_DC_PSW : 8;   // entries per load batch (DC: registers)
+    constexpr int KB = VTK_DC_KB;   // basis vectors per load batch (DC)
+    constexpr int JB = VTK_DC_JB;   // basis vectors with per-lane register accumulators (DC)
     constexpr bool DC = EPI == EPI_PREC_DC;
+    constexpr bool HOIST = DC && VTK_DC_HOIST;
+    constexpr bool WLATE = DC && VTK_DC_WLATE;
     constexpr int NQW = 2 * DC_MAXJ + 3;      // per-wave partial record (DC)
     __shared__ double stage[(NT / 64) * NQW];
     __shared__ double red[NT / 64];
@@ -499,38 +520,77 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         double sub = 0.0, sup = 0.0;   // TRI: the row's block sub/super-diagonal entries
         constexpr bool TRIM = TRI && BS > 0;
         [[maybe_unused]] const int ii = lane & (BS > 0 ? BS - 1 : 0);
+        // HOIST: the row's own operands (BJ factor, p) issued ahead of the CSR loads
+        double mrow = 1.0, pv = 0.0;
+        if constexpr (HOIST) {
+            if (act) {
+                if constexpr (TRIM) mrow = a.tri[a.tri_ld + row];
+                pv = a.x[row];
+            }
+        }
         if (64 * q < a.n_local) {
             const int64_t o0 = a.sell_off[q];
             const int w = (int)((a.sell_off[q + 1] - o0) >> 6);
-            const int32_t *cc = a.sell_col + o0 + lane;
             const VT *vv = a.sell_val + o0 + lane;
-            for (int k0 = 0; k0 < w; k0 += SW) {
-                int c[SW];
-                double d[SW];
+            // products of one batch, summed serially in stored order (padding skipped)
+            auto batch = [&](const auto &c, const auto &d) {
+                constexpr int NB = sizeof(c) / sizeof(c[0]);
+                double xv[NB];
 #pragma unroll
-                for (int u = 0; u < SW; ++u) {
-                    const bool ok = k0 + u < w;
-                    c[u] = ok ? __builtin_nontemporal_load(cc + (k0 + u) * 64) : -1;
-                    d[u] = ok ? (double)__builtin_nontemporal_load(vv + (k0 + u) * 64) : 0.0;
-                }
-                double xv[SW];
+                for (int u = 0; u < NB; ++u) xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
 #pragma unroll
-                for (int u = 0; u < SW; ++u) xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
-#pragma unroll
-                for (int u = 0; u < SW; ++u)
+                for (int u = 0; u < NB; ++u)
                     if (c[u] >= 0) s += d[u] * xv[u];
                 if constexpr (TRIM) {
 #pragma unroll
-                    for (int u = 0; u < SW; ++u) {
+                    for (int u = 0; u < NB; ++u) {
                         if (c[u] == row - 1 && ii > 0) sub = sub + d[u];
                         if (c[u] == row + 1 && ii < BS - 1) sup = sup + d[u];
                     }
                 }
+            };
+            // columns: dictionary codes (one 32-bit word per 8 entries of a lane), or int32
+            // for "wide" chunks / unpacked copies; wave-uniform choice, one code path
+            bool wide = true;
+            int dv = 0;
+            if (a.pk) {   // the chunk's dictionary: one 64-B load by lanes 0..15
+                dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
+                wide = __shfl(dv, 15, 64) != 0;
+            }
+            const int32_t *cc = a.sell_col + o0 + lane;
+            const uint32_t *pw = wide ? nullptr : a.pk + a.pk_off[q] + lane;
+            for (int k0 = 0; k0 < w; k0 += 8) {
+                const uint32_t word = wide ? 0u : __builtin_nontemporal_load(pw + (k0 >> 3) * 64);
+#pragma unroll
+                for (int h = 0; h < 8; h += PSW) {
+                    if (k0 + h >= w) break;   // wave-uniform
+                    int c[PSW];
+                    double d[PSW];
+                    if (wide) {
+#pragma unroll
+                        for (int u = 0; u < PSW; ++u) {
+                            const int k = k0 + h + u;
+                            c[u] = (h + u < 8 && k < w) ? __builtin_nontemporal_load(cc + k * 64) : -1;
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < PSW; ++u) {
+                            const int code = h + u < 8 ? (int)((word >> (4 * (h + u))) & 15u) : PK_CODES;
+                            const int off = __shfl(dv, code, 64);
+                            c[u] = code != PK_CODES ? row + off : -1;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < PSW; ++u)
+                        d[u] = c[u] >= 0 ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
+                    batch(c, d);
+                }
             }
         }
-        const double z = row_epilogue<VT, HALO, EPI, BS, TRI, TRIM>(a, s, row, act, lane, acc0, acc1, sub, sup);
+        const double z = row_epilogue<VT, HALO, EPI, BS, TRI, TRIM>(a, s, row, act, lane, acc0, acc1, sub, sup,
+                                                                    HOIST && TRIM, mrow, !WLATE);
         if constexpr (DC) {
-            const double pv = act ? a.x[row] : 0.0;   // p_j (= the SpMV input) on this row
+            if constexpr (!HOIST) pv = act ? a.x[row] : 0.0;   // p_j (= the SpMV input) on this row
             daa += pv * pv;
             dab += pv * z;
             dag += z * z;
@@ -566,6 +626,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         }
                     }
                 }
+            }
+            if constexpr (WLATE) {
+                if (act) a.y[row] = z;
             }
         }
     }
@@ -660,6 +723,79 @@ hipError_t launch_sell_build(const int32_t *indptr, const int32_t *indices, cons
     return hipGetLastError();
 }
 
+// Dictionary coding of a SELL chunk's columns: one wavefront per chunk collects the distinct
+// offsets (col - row) of its entries in first-seen order (entry-major, lane-minor) into a
+// dictionary of at most PK_CODES, held by lanes 0..14; each entry becomes a 4-bit code, eight
+// per 32-bit word.  A chunk with more offsets keeps its int32 columns (dict[16q+15] = 1).
+// Stencil operators have a handful of offsets per chunk: the 2D Vlasov operator 5 (+2 at the
+// periodic x wrap), 4D 9 (+ wraps) -- 4 B of columns per entry become 0.5 B + 1 B per row.
+__global__ __launch_bounds__(NT) void k_pk_width(const int64_t *__restrict__ off, int64_t nch, int64_t *__restrict__ w64) {
+    for (int64_t q = (int64_t)blockIdx.x * NT + threadIdx.x; q <= nch; q += (int64_t)gridDim.x * NT) {
+        const int64_t w = q < nch ? (off[q + 1] - off[q]) >> 6 : 0;
+        w64[q] = 64 * ((w + 7) / 8);
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_sell_pack(const int64_t *__restrict__ off, const int64_t *__restrict__ pkoff,
+                                                  const int32_t *__restrict__ col, int64_t nch,
+                                                  uint32_t *__restrict__ pk, int32_t *__restrict__ dict,
+                                                  unsigned long long *wide_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * NT) >> 6;
+    for (int64_t q = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 6; q < nch; q += nw) {
+        const int64_t o0 = off[q];
+        const int w = (int)((off[q + 1] - o0) >> 6);
+        const int64_t row = q * 64 + lane;
+        uint32_t *pw = pk + pkoff[q] + lane;
+        int dl = 0, nd = 0;   // lane d < nd holds dictionary entry d
+        bool wide = false;    // wave-uniform
+        uint32_t word = 0xFFFFFFFFu;
+        for (int k = 0; k < w && !wide; ++k) {
+            const int32_t c = col[o0 + 64 * (int64_t)k + lane];
+            const bool valid = c >= 0;
+            const int o = valid ? (int)(c - row) : 0;   // both in [0, 2^31): fits
+            int code = PK_CODES;
+            for (int d = 0; d < nd; ++d) {
+                const int dv = __shfl(dl, d, 64);
+                if (valid && code == PK_CODES && dv == o) code = d;
+            }
+            for (;;) {
+                const unsigned long long pend = __ballot(valid && code == PK_CODES);
+                if (pend == 0) break;
+                if (nd == PK_CODES) { wide = true; break; }
+                const int v = __shfl(o, __ffsll((long long)pend) - 1, 64);
+                if (lane == nd) dl = v;
+                if (valid && code == PK_CODES && o == v) code = nd;
+                ++nd;
+            }
+            const int sh = 4 * (k & 7);
+            word = (word & ~(15u << sh)) | ((uint32_t)code << sh);
+            if ((k & 7) == 7 || k == w - 1) {
+                pw[(int64_t)(k >> 3) * 64] = word;
+                word = 0xFFFFFFFFu;
+            }
+        }
+        if (lane < 16) dict[q * 16 + lane] = lane < nd ? dl : (lane == 15 && wide ? 1 : 0);
+        if (lane == 0 && wide) {
+            atomicAdd(wide_cnt, 1ull);
+            atomicAdd(wide_cnt + 1, 64ull * (unsigned long long)w);
+        }
+    }
+}
+
+hipError_t launch_sell_pack(const int64_t *off, int64_t nch, int64_t *pkoff, int64_t *tmp64, void *scan_tmp,
+                            size_t scan_bytes, const int32_t *col, uint32_t *pk, int32_t *dict,
+                            unsigned long long *wide_cnt, int phase, hipStream_t s) {
+    if (phase == 0) {
+        hipLaunchKernelGGL(k_pk_width, dim3(1024), dim3(NT), 0, s, off, nch, tmp64);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, tmp64, pkoff, (int)(nch + 1), s);
+    }
+    hipLaunchKernelGGL(k_sell_pack, dim3(4096), dim3(NT), 0, s, off, pkoff, col, nch, pk, dict, wide_cnt);
+    return hipGetLastError();
+}
+
 size_t sell_scan_bytes(int64_t n) {
     const int64_t nch = (n + 63) / 64;
     size_t bytes = 0;
@@ -715,7 +851,9 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       y, b, bj.inv, v0, part0, part1, stop_col, col, bj.tri, bj.tri_ld, nullptr, 0, 0, nullptr,
                       sell ? in.sell->d_off : nullptr, sell ? in.sell->d_col : nullptr,
                       sell ? static_cast<const VT *>(in.sell->d_val) : nullptr,
-                      sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0};
+                      sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0,
+                      sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
+                      sell ? in.sell->d_dict : nullptr};
     return a;
 }
 

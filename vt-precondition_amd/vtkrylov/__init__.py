@@ -178,18 +178,27 @@ class CsrOperator:
     def handle(self):
         return self._h
 
-    LAYOUTS = {"auto": 0, "csr": 1, "sell": 2}
+    LAYOUTS = {"auto": 0, "csr": 1, "sell": 2, "sell32": 3}
 
     def set_layout(self, layout: str):
-        """SpMV layout: "sell" (SELL-64 copy), "csr" (CSR-stream tiles) or "auto" (SELL when
-        its padding is <= 25 % of nnz).  Results are bit-identical either way."""
+        """SpMV layout: "sell" (SELL-64 copy, columns dictionary-coded per 64-row chunk),
+        "sell32" (SELL-64 with int32 columns), "csr" (CSR-stream tiles) or "auto" ("sell" when
+        its padding is <= 25 % of nnz).  Results are bit-identical in every layout."""
         check(lib().vtk_csr_set_layout(self._h, self.LAYOUTS[layout]), self.ctx.handle)
 
     @property
     def layout(self) -> str:
         v = C.c_int()
         check(lib().vtk_csr_get_layout(self._h, C.byref(v)), self.ctx.handle)
-        return {1: "csr", 2: "sell"}[v.value]
+        return {1: "csr", 2: "sell", 3: "sell32"}[v.value]
+
+    def layout_info(self) -> dict:
+        """Layout in use, bytes of the operator one SpMV reads in it, SELL chunk counts."""
+        li = _abi.LayoutInfo()
+        check(lib().vtk_csr_layout_info(self._h, C.byref(li)), self.ctx.handle)
+        d = {k: getattr(li, k) for k, _ in li._fields_}
+        d["layout"] = {1: "csr", 2: "sell", 3: "sell32"}[d["layout"]]
+        return d
 
     def matvec(self, x):
         """y = A x on this rank's rows (sparsetools csr_matvec, bit-identical)."""

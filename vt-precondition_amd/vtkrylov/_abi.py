@@ -83,6 +83,7 @@ PROTOTYPES = {
     "vtk_bjacobi_set_mode": (C.c_int, [P, C.c_int]),
     "vtk_csr_set_layout": (C.c_int, [P, C.c_int]),
     "vtk_csr_get_layout": (C.c_int, [P, C.POINTER(C.c_int)]),
+    "vtk_csr_layout_info": (C.c_int, [P, C.c_void_p]),
     "vtk_bjacobi_get_mode": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_destroy": (None, [P]),
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
@@ -91,6 +92,11 @@ PROTOTYPES = {
     "vtk_profile_enable": (C.c_int, [P, C.c_int]),
     "vtk_profile_read": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_int)]),
 }
+
+
+class LayoutInfo(C.Structure):
+    _fields_ = [("layout", C.c_int), ("matrix_bytes", C.c_double), ("sell_chunks", C.c_int64),
+                ("sell_entries", C.c_int64), ("wide_chunks", C.c_int64)]
 
 
 class KernelProfile(C.Structure):
