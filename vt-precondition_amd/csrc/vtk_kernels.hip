@@ -482,6 +482,12 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_DC_JB
 #define VTK_DC_JB 10
 #endif
+#ifndef VTK_VAL_EARLY
+#define VTK_VAL_EARLY 1
+#endif
+#ifndef VTK_SCALAR_Q
+#define VTK_SCALAR_Q 1
+#endif
 #ifndef VTK_DC_PSW
 #define VTK_DC_PSW 4
 #endif
@@ -513,7 +519,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     for (int t = blockIdx.x; t < a.ngroups; t += gridDim.x) {
         const int g = a.group_list ? a.group_list[t] : t;
-        const int q = 4 * g + wv;
+        const int q = VTK_SCALAR_Q ? __builtin_amdgcn_readfirstlane(4 * g + wv) : 4 * g + wv;
         const int row = 64 * q + lane;
         const bool act = row < a.n_local;
         double s = 0.0;
@@ -580,9 +586,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                             c[u] = code != PK_CODES ? row + off : -1;
                         }
                     }
+                    // values do not wait for the codes: padding slots hold 0 and are skipped
 #pragma unroll
                     for (int u = 0; u < PSW; ++u)
-                        d[u] = c[u] >= 0 ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
+                        d[u] = (VTK_VAL_EARLY ? (h + u < 8 && k0 + h + u < w) : c[u] >= 0)
+                                   ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
                     batch(c, d);
                 }
             }
