@@ -55,6 +55,12 @@ def lib():
         L.orc_gmres.argtypes = [C.c_int64, P, P, P, C.c_int, P, C.c_int, P, P, C.c_double,
                                 C.c_double, C.c_int, C.c_int64, C.POINTER(C.c_int),
                                 C.POINTER(_Stats)]
+        L.orc_line_setup.argtypes = [C.c_int64, P, P, P, C.c_int, C.c_int64, C.c_int64, C.c_int64, P]
+        L.orc_line_setup.restype = C.c_int64
+        L.orc_line_apply.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int64, P, P, P]
+        L.orc_gmres_line.argtypes = [C.c_int64, P, P, P, C.c_int, P, C.c_int64, C.c_int64, P, P,
+                                     C.c_double, C.c_double, C.c_int, C.c_int64,
+                                     C.POINTER(C.c_int), C.POINTER(_Stats)]
         _lib = L
     return _lib
 
@@ -114,6 +120,32 @@ def bj_apply(inv, r):
     return z
 
 
+class LineFactors:
+    """Line-Jacobi factors ``f = [l | m | g]`` of rows [row0, row0+n) (orc_line_setup)."""
+
+    def __init__(self, f, row0: int, stride: int, seg: int):
+        self.f, self.row0, self.stride, self.seg = f, row0, stride, seg
+
+
+def line_setup(indptr, indices, data, stride: int, seg: int, row0: int = 0) -> LineFactors:
+    """``indices`` are GLOBAL columns of the row block [row0, row0 + n)."""
+    n = indptr.shape[0] - 1
+    f = np.empty(3 * max(n, 1), np.float64)[:3 * n]
+    rc = lib().orc_line_setup(n, _ptr(indptr), _ptr(indices), _ptr(data),
+                              int(data.dtype == np.float32), row0, stride, seg, _ptr(f))
+    if rc != 0:
+        raise np.linalg.LinAlgError(f"zero or non-finite line pivot at row {row0 - rc - 1}")
+    return LineFactors(f, row0, stride, seg)
+
+
+def line_apply(lf: LineFactors, r):
+    n = r.shape[0]
+    z = np.empty(n, np.float64)
+    lib().orc_line_apply(n, lf.row0, lf.stride, lf.seg, _ptr(lf.f),
+                         _ptr(np.ascontiguousarray(r, np.float64)), _ptr(z))
+    return z
+
+
 def lartg(f: float, g: float):
     c, s, r = C.c_double(), C.c_double(), C.c_double()
     lib().orc_lartg(f, g, C.byref(c), C.byref(s), C.byref(r))
@@ -132,8 +164,17 @@ class Solve:
 
 def gmres(indptr, indices, data, b, inv=None, *, x0=None, rtol=1e-5, atol=0.0, restart=20,
           maxiter=None) -> Solve:
+    """``inv``: None, block inverses (bj_setup) or LineFactors (line_setup, row0 = 0)."""
     n = b.shape[0]
     x = np.zeros(n) if x0 is None else np.array(x0, np.float64, copy=True)
+    if isinstance(inv, LineFactors):
+        info = C.c_int()
+        st = _Stats()
+        lib().orc_gmres_line(n, _ptr(indptr), _ptr(indices), _ptr(data), int(data.dtype == np.float32),
+                             _ptr(inv.f), inv.stride, inv.seg, _ptr(np.ascontiguousarray(b, np.float64)),
+                             _ptr(x), rtol, atol, restart, 0 if maxiter is None else maxiter,
+                             C.byref(info), C.byref(st))
+        return Solve(x, info.value, st.inner_iters, st.restarts, st.presid, st.rnorm)
     bs = 0 if inv is None else inv.shape[1]
     info = C.c_int()
     st = _Stats()

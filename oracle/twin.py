@@ -301,6 +301,98 @@ def bj_operator(Binv, n):
                           dtype=np.float64)
 
 
+# ---------------------------------------------------------------------------------------
+# Line Jacobi: x-direction line segments.  M keeps A's diagonal and the
+# couplings of rows R, R +- stride whose line index R // stride lies in the same segment of
+# `seg` consecutive lines, both rows in [row0, row0 + n).  Restated from the definition
+# (SciPy: splu of that matrix) and as the Thomas sweeps oracle/vtk_oracle.c orc_line_setup /
+# orc_line_apply perform (same IEEE operation order: bit-identical to the C restatement).
+# ---------------------------------------------------------------------------------------
+
+
+def _line_geometry(indptr, indices, n, stride, seg, row0):
+    ip = np.asarray(indptr, dtype=np.int64)
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(ip)) + row0
+    cols = np.asarray(indices, dtype=np.int64)
+    R = np.arange(row0, row0 + n, dtype=np.int64)
+
+    def has(d):
+        Q = R + d * stride
+        return (Q >= row0) & (Q < row0 + n) & ((Q // stride) // seg == (R // stride) // seg)
+
+    return rows, cols, R, has(-1), has(1)
+
+
+def line_matrix(indptr, indices, data, n, stride, seg, row0=0):
+    """M as a SciPy CSR matrix (duplicates summed as toarray() does)."""
+    import scipy.sparse as sp
+    rows, cols, R, hl, hr = _line_geometry(indptr, indices, n, stride, seg, row0)
+    r = rows - row0
+    keep = (cols == rows) | ((cols == rows - stride) & hl[r]) | ((cols == rows + stride) & hr[r])
+    M = sp.coo_matrix((np.asarray(data, np.float64)[keep], (r[keep], cols[keep] - row0)), shape=(n, n))
+    return M.tocsr()
+
+
+def line_factors_numpy(indptr, indices, data, n, stride, seg, row0=0):
+    """Thomas factors f = [l | m | g] (vectorised over the lines, ascending line index)."""
+    rows, cols, R, hl, hr = _line_geometry(indptr, indices, n, stride, seg, row0)
+    v = np.asarray(data, np.float64)
+    r = rows - row0
+    b = np.zeros(n); a = np.zeros(n); c = np.zeros(n)
+    mb = cols == rows
+    ma = ~mb & (cols == rows - stride) & hl[r]
+    mc = ~mb & ~ma & (cols == rows + stride) & hr[r]
+    np.add.at(b, r[mb], v[mb])          # unbuffered: stored order, from 0.0
+    np.add.at(a, r[ma], v[ma])
+    np.add.at(c, r[mc], v[mc])
+    l = np.zeros(n); u = np.zeros(n); m = np.zeros(n); g = np.zeros(n)
+    i_lo, i_hi = row0 // stride, (row0 + n - 1) // stride
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for i in range(i_lo, i_hi + 1):
+            lo, hi = max(i * stride, row0) - row0, min((i + 1) * stride, row0 + n) - row0
+            k = np.arange(lo, hi)
+            first = ~hl[k]
+            kp = np.where(first, k, k - stride)
+            lv = np.where(first, 0.0, a[k] / u[kp])
+            uv = np.where(first, b[k], b[k] - lv * np.where(first, 0.0, c[kp]))
+            u[k] = uv
+            l[k] = lv
+            m[k] = 1.0 / uv
+            g[k] = c[k] * m[k]
+    bad = (u == 0) | ~np.isfinite(u) | ~np.isfinite(m)
+    if n and bad.any():
+        raise np.linalg.LinAlgError(f"zero or non-finite line pivot at row {row0 + int(np.argmax(bad))}")
+    return np.concatenate([l, m, g])
+
+
+def line_apply_numpy(f, r, stride, seg, row0=0):
+    n = r.shape[0]
+    l, m, g = f[:n], f[n:2 * n], f[2 * n:]
+    R = np.arange(row0, row0 + n, dtype=np.int64)
+    same = lambda d: ((R + d * stride >= row0) & (R + d * stride < row0 + n)
+                      & (((R + d * stride) // stride) // seg == (R // stride) // seg))
+    hl, hr = same(-1), same(1)
+    d = np.zeros(n); z = np.zeros(n)
+    i_lo, i_hi = row0 // stride, (row0 + n - 1) // stride
+    sl = [np.arange(max(i * stride, row0) - row0, min((i + 1) * stride, row0 + n) - row0)
+          for i in range(i_lo, i_hi + 1)]
+    for k in sl:
+        dp = np.where(hl[k], d[np.maximum(k - stride, 0)], 0.0)
+        d[k] = r[k] - l[k] * dp
+    for k in reversed(sl):
+        zn = np.where(hr[k], z[np.minimum(k + stride, n - 1)], 0.0)
+        z[k] = m[k] * d[k] - g[k] * zn
+    return z
+
+
+def line_operator(indptr, indices, data, n, stride, seg):
+    """SciPy statement of the preconditioner: a LinearOperator solving with splu(M)."""
+    from scipy.sparse.linalg import LinearOperator, splu
+    lu = splu(line_matrix(indptr, indices, data, n, stride, seg).tocsc(), permc_spec="NATURAL")
+    return LinearOperator((n, n), matvec=lambda r: lu.solve(np.asarray(r, np.float64).reshape(-1)),
+                          dtype=np.float64)
+
+
 @dataclass
 class ScipySolve:
     x: np.ndarray
@@ -319,7 +411,10 @@ def scipy_gmres(A, b, Binv=None, *, rtol=1e-8, atol=0.0, restart=20, maxiter=Non
     import time
     from scipy.sparse.linalg import gmres
     n = b.shape[0]
-    M = bj_operator(Binv, n) if Binv is not None else None
+    if Binv is None or hasattr(Binv, "matvec"):
+        M = Binv                      # None or a LinearOperator (e.g. line_operator)
+    else:
+        M = bj_operator(Binv, n)
     count = [0]
 
     def cb(_):

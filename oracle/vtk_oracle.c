@@ -253,6 +253,73 @@ void orc_lartg(double f, double g, double *c, double *s, double *r) {
     }
 }
 
+/* ---- line Jacobi (line-implicit x-direction preconditioner) -------------
+ * M keeps A's diagonal and the couplings between global rows R and R +- stride whose line
+ * index i = R / stride falls in the same segment i / seg, both rows inside [row0, row0 + n).
+ * Each (segment, j = R mod stride) is a tridiagonal system along its line; Thomas without
+ * pivoting over the line in ascending i:
+ *   u = b (first row) | l = a / u_prev, u = b - l * c_prev;   m = 1 / u;   g = c * m
+ * with b, a, c the sums (stored order, from 0.0: toarray() semantics) of the row's entries in
+ * columns R, R - stride, R + stride.  f = [l | m | g], n doubles each (l = 0 on first rows).
+ * The HIP setup (vtk_kernels.hip k_line_setup) runs the same IEEE operations per line. */
+static int line_has(int64_t R, int64_t d, int64_t row0, int64_t n, int64_t stride, int64_t seg) {
+    const int64_t Q = R + d * stride;
+    return Q >= row0 && Q < row0 + n && (Q / stride) / seg == (R / stride) / seg;
+}
+
+int64_t orc_line_setup(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
+                       int fp32, int64_t row0, int64_t stride, int64_t seg, double *f) {
+    double *u = (double *)malloc(sizeof(double) * (n ? n : 1));
+    double *cs = (double *)malloc(sizeof(double) * (n ? n : 1));
+    double *l = f, *mm = f + n, *g = f + 2 * n;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t R = row0 + r;
+        const int hl = line_has(R, -1, row0, n, stride, seg), hr = line_has(R, 1, row0, n, stride, seg);
+        double b = 0.0, a = 0.0, c = 0.0;
+        for (int32_t k = indptr[r]; k < indptr[r + 1]; ++k) {
+            const int64_t col = indices[k];
+            const double v = val_at(data, fp32, k);
+            if (col == R) b += v;
+            else if (hl && col == R - stride) a += v;
+            else if (hr && col == R + stride) c += v;
+        }
+        double lv = 0.0, uv;
+        if (hl) {
+            lv = a / u[r - stride];
+            uv = b - lv * cs[r - stride];
+        } else {
+            uv = b;
+        }
+        const double mv = 1.0 / uv;
+        if (uv == 0.0 || !isfinite(uv) || !isfinite(mv)) { free(u); free(cs); return -(r + 1); }
+        u[r] = uv;
+        cs[r] = c;
+        l[r] = lv;
+        mm[r] = mv;
+        g[r] = c * mv;
+    }
+    free(u);
+    free(cs);
+    return 0;
+}
+
+/* z = M^-1 r: forward d = r - l d_prev (d_prev = 0 on a first row), backward
+ * z = m d - g z_next (z_next = 0 on a last row) */
+void orc_line_apply(int64_t n, int64_t row0, int64_t stride, int64_t seg, const double *f,
+                    const double *r, double *z) {
+    const double *l = f, *mm = f + n, *g = f + 2 * n;
+    double *d = (double *)malloc(sizeof(double) * (n ? n : 1));
+    for (int64_t i = 0; i < n; ++i) {
+        const double dp = line_has(row0 + i, -1, row0, n, stride, seg) ? d[i - stride] : 0.0;
+        d[i] = r[i] - l[i] * dp;
+    }
+    for (int64_t i = n - 1; i >= 0; --i) {
+        const double zn = line_has(row0 + i, 1, row0, n, stride, seg) ? z[i + stride] : 0.0;
+        z[i] = mm[i] * d[i] - g[i] * zn;
+    }
+    free(d);
+}
+
 static double dot(int64_t n, const double *a, const double *b) {
     double s = 0.0;
     for (int64_t i = 0; i < n; ++i) s += a[i] * b[i];
@@ -267,20 +334,41 @@ typedef struct {
     int fp32;
     const double *inv;
     int bs;
+    const double *line;   /* line-Jacobi factors (orc_line_setup), row0 = 0 */
+    int64_t stride, seg;
 } op_t;
 
 static void matvec(const op_t *o, const double *x, double *y) {
     orc_spmv(o->n, o->indptr, o->indices, o->data, o->fp32, x, y);
 }
 static void psolve(const op_t *o, const double *r, double *z) {
-    if (o->inv) orc_bj_apply(o->n, o->bs, o->inv, r, z);
+    if (o->line) orc_line_apply(o->n, 0, o->stride, o->seg, o->line, r, z);
+    else if (o->inv) orc_bj_apply(o->n, o->bs, o->inv, r, z);
     else memcpy(z, r, sizeof(double) * o->n);
 }
+
+static int gmres_op(const op_t *op, const double *b, double *x, double rtol, double atol,
+                    int restart, int64_t maxiter, int *info, orc_stats *st);
 
 int orc_gmres(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
               int fp32, const double *bj_inv, int bs, const double *b, double *x, double rtol,
               double atol, int restart, int64_t maxiter, int *info, orc_stats *st) {
-    op_t o = {n, indptr, indices, data, fp32, bj_inv, bs};
+    op_t o = {n, indptr, indices, data, fp32, bj_inv, bs, NULL, 0, 0};
+    return gmres_op(&o, b, x, rtol, atol, restart, maxiter, info, st);
+}
+
+int orc_gmres_line(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
+                   int fp32, const double *line_f, int64_t stride, int64_t seg, const double *b,
+                   double *x, double rtol, double atol, int restart, int64_t maxiter, int *info,
+                   orc_stats *st) {
+    op_t o = {n, indptr, indices, data, fp32, NULL, 0, line_f, stride, seg};
+    return gmres_op(&o, b, x, rtol, atol, restart, maxiter, info, st);
+}
+
+static int gmres_op(const op_t *op, const double *b, double *x, double rtol, double atol,
+                    int restart, int64_t maxiter, int *info, orc_stats *st) {
+    const op_t o = *op;
+    const int64_t n = o.n;
     memset(st, 0, sizeof(*st));
     double bnrm2 = nrm2(n, b);
     double rb = rtol * bnrm2;                        /* _get_atol_rtol :19 */

@@ -41,6 +41,14 @@ int64_t orc_bj_setup(int64_t n, const int32_t *indptr, const int32_t *indices, c
 void orc_bj_apply(int64_t n, int bs, const double *inv, const double *r, double *z);
 void orc_lartg(double f, double g, double *c, double *s, double *r);
 
+/* line Jacobi (x-direction line segments): factors f = [l | m | g] (3n
+ * doubles) of the rows [row0, row0+n) with GLOBAL column indices; returns 0 or -(row+1) when a
+ * pivot is zero or not finite.  apply: z = M^-1 r. */
+int64_t orc_line_setup(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
+                       int fp32, int64_t row0, int64_t stride, int64_t seg, double *f);
+void orc_line_apply(int64_t n, int64_t row0, int64_t stride, int64_t seg, const double *f,
+                    const double *r, double *z);
+
 typedef struct {
     int64_t inner_iters;
     int64_t restarts;
@@ -52,6 +60,12 @@ typedef struct {
 int orc_gmres(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
               int fp32, const double *bj_inv, int bs, const double *b, double *x, double rtol,
               double atol, int restart, int64_t maxiter, int *info, orc_stats *st);
+
+/* the same GMRES with the line-Jacobi preconditioner (factors of orc_line_setup, row0 = 0) */
+int orc_gmres_line(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
+                   int fp32, const double *line_f, int64_t stride, int64_t seg, const double *b,
+                   double *x, double rtol, double atol, int restart, int64_t maxiter, int *info,
+                   orc_stats *st);
 
 #ifdef __cplusplus
 }

@@ -33,6 +33,12 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_line():
+    with np.load(os.path.join(GOLDEN, "golden_line.npz"), allow_pickle=False) as g:
+        return {k: g[k] for k in g.files}
+
+
+@pytest.fixture(scope="session")
 def golden_large():
     with open(os.path.join(GOLDEN, "golden_large.json")) as f:
         return json.load(f)

@@ -7,6 +7,8 @@
 Outputs (all data, no code):
   golden_small.npz  — vectors for C0, S2, S4, S4F, a ragged random CSR, GMRES edge cases
   golden_large.json — SHA-256 of the C1..C4 CSR byte streams, ||A·1||, SciPy GMRES summary
+  golden_line.npz   — line-Jacobi solves (SciPy splu of M) and SciPy GMRES with it (--line-only,
+                      which also adds the C1 line-GMRES summary to golden_large.json)
 """
 from __future__ import annotations
 
@@ -119,6 +121,55 @@ def small(out):
     print("wrote", out, os.path.getsize(out), "bytes")
 
 
+LINE_SEG = 25   # x-points per line segment (divides Nx / 8 of C1..C4)
+
+
+def line_stride(p) -> int:
+    """Rows between x-neighbours: 1 (1D), Nv (2D), Ny*Nvx*Nvy (4D)."""
+    return 1 if p.dim == 1 else (p.shape[1] if p.dim == 2 else p.n // p.shape[0])
+
+
+def line(out, out_json):
+    """Line-Jacobi fixtures: SciPy splu solves with M and SciPy GMRES with
+    that LinearOperator, on the small configs, a ragged random CSR and C1 (summary)."""
+    g = {}
+    cases = [(name, twin.CONFIGS[name]) for name in ["C0", "S2", "S4", "S4F"]]
+    for name, p in cases:
+        ip, ix, d = twin.generate(p)
+        A = twin.scipy_csr(ip, ix, d, p.n)
+        b = twin.rhs(p.n)
+        st = line_stride(p)
+        for seg in (3, LINE_SEG):
+            M = twin.line_operator(ip, ix, d, p.n, st, seg)
+            g[f"{name}/line{seg}_z"] = M.matvec(b)
+        s = twin.scipy_gmres(A, b, twin.line_operator(ip, ix, d, p.n, st, LINE_SEG), rtol=1e-8)
+        g[f"{name}/gmres_line_x"] = s.x
+        g[f"{name}/gmres_line_meta"] = np.array([s.info, s.inner_iters, s.true_resid, s.b_norm])
+        print(name, "line gmres info", s.info, "inner", s.inner_iters)
+    R = ragged_csr()
+    n = R.shape[0]
+    M = twin.line_operator(R.indptr, R.indices, R.data, n, 37, 5)
+    g["ragged/line37_5_z"] = M.matvec(twin.rhs(n))
+    # non-canonical rows: duplicates and unsorted columns add up as toarray() does
+    np.savez_compressed(out, **g)
+    print("wrote", out, os.path.getsize(out), "bytes")
+    with open(out_json) as f:
+        res = json.load(f)
+    p = twin.CONFIGS["C1"]
+    ip, ix, d = twin.generate(p)
+    A = twin.scipy_csr(ip, ix, d, p.n)
+    b = twin.rhs(p.n)
+    s = twin.scipy_gmres(A, b, twin.line_operator(ip, ix, d, p.n, line_stride(p), LINE_SEG), rtol=1e-8)
+    print("C1 line gmres", s.info, s.inner_iters)
+    res["C1"][f"gmres_line{LINE_SEG}"] = {
+        "rtol": 1e-8, "restart": 20, "stride": line_stride(p), "seg": LINE_SEG, "info": s.info,
+        "inner_iters": s.inner_iters, "x_norm2": float(np.linalg.norm(s.x)),
+        "true_resid": s.true_resid, "b_norm2": s.b_norm, "x_first8": s.x[:8].tolist()}
+    with open(out_json, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print("wrote", out_json)
+
+
 def large(out, with_c4):
     res = {}
     if os.path.exists(out):
@@ -163,7 +214,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--skip-small", action="store_true")
+    ap.add_argument("--line-only", action="store_true", help="only the line-Jacobi fixtures")
     a = ap.parse_args()
+    if a.line_only:
+        line(os.path.join(HERE, "golden_line.npz"), os.path.join(HERE, "golden_large.json"))
+        sys.exit(0)
     if not a.skip_small:
         small(os.path.join(HERE, "golden_small.npz"))
     large(os.path.join(HERE, "golden_large.json"), a.c4)
