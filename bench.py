@@ -58,7 +58,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit):
+def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit, line=None):
     """SciPy 1.15.3 (the reference scipy.sparse path) on the host cores, bounded sample."""
     import numpy as np
     import scipy.sparse as sp
@@ -79,14 +79,17 @@ def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit):
     for _ in range(reps):
         A @ x
     t_spmv = (time.perf_counter() - t) / reps
-    Binv = twin.bj_inverse_numpy(ip, ix, d, n, bs)
-    s = twin.scipy_gmres(A, b, Binv, rtol=rtol, inner_limit=inner_limit)
+    if line is None:
+        Mop, mname = twin.bj_inverse_numpy(ip, ix, d, n, bs), f"BJ({bs})"
+    else:   # (stride, seg): SciPy's splu of the line matrix as the LinearOperator
+        Mop, mname = twin.line_operator(ip, ix, d, n, line[0], line[1]), f"Line(stride={line[0]}, seg={line[1]}) splu"
+    s = twin.scipy_gmres(A, b, Mop, rtol=rtol, inner_limit=inner_limit)
     return {
         "value": s.inner_iters / s.seconds,
         "unit": "iters/s",
         "cores": int(blas_threads),
         "kind": "reference",
-        "sample": (f"scipy.sparse.linalg.gmres(restart=20, M=BJ({bs}) LinearOperator) on the same "
+        "sample": (f"scipy.sparse.linalg.gmres(restart=20, M={mname} LinearOperator) on the same "
                    f"{cfg_name} operator/RHS, first {s.inner_iters} inner iterations (one restart "
                    f"cycle, legacy maxiter bound) in {s.seconds:.1f} s; csr_matvec is single-threaded, "
                    f"np.dot uses {blas_threads} BLAS threads; host cpus in affinity: "
@@ -116,6 +119,10 @@ def main():
     ap.add_argument("--layout", default="auto", choices=["auto", "sell", "sell32", "csr"],
                     help="SpMV layout: auto (SELL-64 when its padding is small), sell (dictionary-coded "
                          "columns), sell32 (int32 columns), csr (CSR-stream tiles)")
+    ap.add_argument("--prec", default="bj", choices=["bj", "line"],
+                    help="preconditioner: bj (block-Jacobi(bs), SURVEY §8d, the metric's config) or line "
+                         "(line-Jacobi along x, segments of --seg x-points, SURVEY §8f-4)")
+    ap.add_argument("--seg", type=int, default=25, help="line-Jacobi segment length (x-points)")
     ap.add_argument("--comm-solo", action="store_true",
                     help="one GPU through the distributed code paths (one-rank RCCL communicator)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -160,7 +167,12 @@ def main():
     t0 = time.time()
     A = vk.vlasov_operator(params, ctx=ctx, offsets=offsets)
     A.set_layout(args.layout)
-    M = vk.block_jacobi(A, args.bs, mode=args.bj_mode)
+    if args.prec == "line":
+        M = vk.line_jacobi(A, vk.vlasov_line_stride(params), args.seg)
+        mdesc, mmode = f"Line({args.seg})", "line"
+    else:
+        M = vk.block_jacobi(A, args.bs, mode=args.bj_mode)
+        mdesc, mmode = f"BJ({args.bs})", M.mode
     b_host = vk.rhs_splitmix(n_glob, r0=A.row_begin, r1=A.row_end)
     b = torch.from_numpy(b_host).to(dev)
     torch.cuda.synchronize()
@@ -282,13 +294,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f64" if not fp32 else "f32-values/f64",
         "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
-        "config": {"workload": f"{args.config}: GMRES({args.restart}, {args.orth})+BJ({args.bs}) to rtol={args.rtol}, "
+        "config": {"workload": f"{args.config}: GMRES({args.restart}, {args.orth})+{mdesc} to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "bs": args.bs, "bj_apply": M.mode, "layout": A.layout, "rtol": args.rtol, "orth": args.orth,
+                   "prec": args.prec, "bs": args.bs if args.prec == "bj" else None,
+                   "seg": args.seg if args.prec == "line" else None, "bj_apply": mmode, "layout": A.layout, "rtol": args.rtol, "orth": args.orth,
                    "parallelism": f"row-slab x{world}",
                    "comm": args.comm if world > 1 else ("rccl-solo" if args.comm_solo else None)},
         "inner_iters_per_solve": iters / args.steps,
+        "solves_per_s": args.steps / elapsed,
         "info": infos,
         "true_rel_residual": rel_res,
         "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B,
@@ -315,7 +329,8 @@ def main():
         try:
             A_host = A.download()
             out["cpu_baseline"] = cpu_baseline(args.config, A_host, b_host, args.bs, args.rtol,
-                                               args.cpu_inner)
+                                               args.cpu_inner,
+                                               (vk.vlasov_line_stride(params), args.seg) if args.prec == "line" else None)
         except Exception as e:  # reported, never silently replaced
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -11,6 +11,8 @@
  *   vtk_spmv            <- csr_matrix @ x -> _matmul_vector (scipy/sparse/_compressed.py:518-530)
  *   vtk_bjacobi_create  <- numpy.linalg.inv on the bs x bs diagonal blocks
  *   vtk_bjacobi_apply   <- LinearOperator(matvec=einsum('bij,bj->bi'))
+ *   vtk_linejacobi_*    <- LinearOperator(matvec=splu(M).solve), M = diagonal + x-line
+ *                          couplings (line-implicit x-direction solve)
  *   vtk_gmres           <- scipy.sparse.linalg.gmres(A, b, x0, rtol=, atol=, restart=,
  *                          maxiter=, M=) (scipy/sparse/linalg/_isolve/iterative.py:582-841)
  * The config/entry layer the reference does have (XML node lookups, ini_info.py:72-118;
@@ -197,6 +199,24 @@ int vtk_bjacobi_set_mode(vtk_prec *M, int mode);
 /* *mode_in_use = VTK_BJ_INVERSE or VTK_BJ_TRIDIAG; *tridiag_available = 0/1 (either may be NULL) */
 int vtk_bjacobi_get_mode(vtk_prec *M, int *mode_in_use, int *tridiag_available);
 void vtk_prec_destroy(vtk_prec *M);
+
+/* ---- line-Jacobi preconditioner --------------------------------------
+ * Line-implicit x-direction preconditioner.  M keeps A's diagonal and the couplings between
+ * global rows R and R +- stride whose line index R / stride lies in the same segment of `seg`
+ * consecutive line indices (segments also end at the rank's row block): every (segment,
+ * R mod stride) is a tridiagonal system along an x-line, factored by Thomas (no pivoting) and
+ * applied by a forward and a backward sweep (24 B of factors per row).  SciPy statement:
+ * splu(M).solve as a LinearOperator.  Vlasov operators: stride 1 (1D), Nv (2D), Ny*Nvx*Nvy
+ * (4D); seg dividing Nx / world makes M independent of the rank count.  VTK_ERR_SINGULAR
+ * when a pivot is zero or not finite.  Apply with vtk_prec_apply (or vtk_bjacobi_apply); use
+ * as vtk_gmres's M. */
+typedef enum { VTK_PREC_BJACOBI = 0, VTK_PREC_LINE = 1 } vtk_prec_kind;
+int vtk_linejacobi_create(vtk_csr *A, int64_t stride, int64_t seg, vtk_prec **out);
+/* export the factors l | m | g (3 * n_local doubles; the oracle's orc_line_setup layout) */
+int vtk_linejacobi_factors(vtk_prec *M, double *f, int ptr_kind);
+/* z = M^-1 r for any preconditioner; *kind = vtk_prec_kind */
+int vtk_prec_apply(vtk_prec *M, const double *r, double *z, int ptr_kind);
+int vtk_prec_kind_of(vtk_prec *M, int *kind);
 
 /* ---- solver --------------------------------------------------------------------------- */
 /* scipy.sparse.linalg.gmres semantics (iterative.py:582-841, callback=None): restarted,

@@ -26,6 +26,9 @@ for s in "$@"; do
         benchq) step benchq 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         benchc4) step benchc4 600 python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 ;;
         benchc2) step benchc2 300 python bench.py --config C2 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        line) step line 900 python -u -m pytest tests/test_gpu_line.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        benchline) step benchline 300 python bench.py --prec line --steps 5 --warmup 1 --no-cpu-baseline ;;
+        benchlinec4) step benchlinec4 600 python bench.py --config C4 --prec line --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 10 ;;
         benchc1) step benchc1 300 python bench.py --config C1 --steps 5 --warmup 1 --no-cpu-baseline ;;
         benchinv) step benchinv 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bj-mode inverse ;;
         benchc4csr) step benchc4csr 600 python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 --layout csr ;;

@@ -126,6 +126,10 @@ void prof_flush(vtk_ctx *c, int last_col = 1 << 30) {
 BjOp bj_op(const vtk_prec *M) {
     BjOp o;
     if (!M) return o;
+    if (M->kind == VTK_PREC_LINE) {
+        o.line = &M->line;
+        return o;
+    }
     o.inv = M->d_inv;
     o.bs = M->bs;
     if (M->tri_ok && M->mode != VTK_BJ_INVERSE) {
@@ -135,9 +139,13 @@ BjOp bj_op(const vtk_prec *M) {
     return o;
 }
 
+// profile class of a standalone preconditioner apply
+const char *prec_cls(const vtk_prec *M) { return M && M->kind == VTK_PREC_LINE ? "line_apply" : "bj_apply"; }
+
 // algorithmic bytes per row of one BJ application (tridiagonal: the SELL kernels read only m)
 double bj_row_bytes(const vtk_prec *M) {
     if (!M) return 0.0;
+    if (M->kind == VTK_PREC_LINE) return 24.0;   // l, m, g
     if (bj_op(M).tri) return M->A->use_sell ? 8.0 : 24.0;
     return 8.0 * M->bs;
 }
@@ -308,7 +316,7 @@ SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nu
 // the fused SpMV + BJ kernels apply: SELL chunks align with any power-of-two bs <= 32; the
 // CSR-stream path needs the BJ tiles aligned and free of long rows
 bool bj_fused(const vtk_prec *M) {
-    if (!M) return false;
+    if (!M || M->kind != VTK_PREC_BJACOBI) return false;
     if (M->A->use_sell) return (M->bs & (M->bs - 1)) == 0 && M->bs <= 32;
     return M->fused;
 }
@@ -618,7 +626,7 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
             Prof pf(c, "spmv", col, b_csr + 2 * n8);
             HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr, nullptr, stop, col, c->stream));
         }
-        Prof pf(c, "bj_apply", col, b_inv + 3 * n8);
+        Prof pf(c, prec_cls(s.M), col, b_inv + 3 * n8);
         HIPCHK(c, launch_bj_apply(bj_op(s.M), s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
         cnt = s.G;
     }
@@ -772,7 +780,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     Red rb = reduce(c, s.part[0], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rb, &ds->scal[0], 1, c->stream));
-    { Prof pf(c, "bj_apply", -1, b_pc);
+    { Prof pf(c, prec_cls(M), -1, b_pc);
       HIPCHK(c, launch_bj_apply(bj_op(M), n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream)); }
     Red rmb = reduce(c, s.part[1], s.G, rc);
     TRY(rc);
@@ -834,7 +842,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);   // :723
     double presid = 0.0;
     const double bytes_spmv = matrix_bytes(A) + 16.0 * n;
-    const double bytes_pc = M ? (8.0 * M->bs * n + 16.0 * n) : 16.0 * n;
+    const double bytes_pc = bj_row_bytes(M) * n + 16.0 * n;
     hipEvent_t ev[LOOKAHEAD + 1];
     for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     struct EvGuard { hipEvent_t *e; ~EvGuard() { for (int i = 0; i <= LOOKAHEAD; ++i) (void)hipEventDestroy(e[i]); } } eg{ev};
@@ -847,7 +855,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         HIPCHK(c, hipMemcpyAsync(&ds->ptol, &hs->ptol, sizeof(double), hipMemcpyHostToDevice, c->stream));
         Red rv = rz;
         if (!fres) {
-            { Prof pf(c, "bj_apply", -1, b_pc);
+            { Prof pf(c, prec_cls(M), -1, b_pc);
               HIPCHK(c, launch_bj_apply(bj_op(M), n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
             rv = reduce(c, s.part[0], s.G, rc);
             TRY(rc);
@@ -1259,9 +1267,59 @@ int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
     return VTK_OK;
 }
 
+int vtk_linejacobi_create(vtk_csr *A, int64_t stride, int64_t seg, vtk_prec **out) {
+    if (!A || !out) return VTK_ERR_ARG;
+    vtk_ctx *c = A->ctx;
+    *out = nullptr;
+    if (stride < 1 || seg < 1) return fail(c, VTK_ERR_ARG, "vtk_linejacobi_create: stride and seg must be >= 1");
+    if (A->n_global > 0 && stride >= A->n_global && A->n_global > 1)
+        return fail(c, VTK_ERR_ARG, "vtk_linejacobi_create: stride must be below n (no line has two rows)");
+    HIPCHK(c, hipSetDevice(c->device));
+    auto *M = new vtk_prec();
+    struct Guard { vtk_prec *&m; ~Guard() { if (m) vtk_prec_destroy(m); } } g{M};
+    M->A = A;
+    M->kind = VTK_PREC_LINE;
+    M->bs = 0;
+    M->line = line_plan(A->n_local, A->row_begin, stride, seg);
+    HIPCHK(c, hipMalloc(&M->line.f, 3 * std::max<int64_t>(A->n_local, 1) * sizeof(double)));
+    DBuf bad;
+    TRY(dalloc(c, bad, sizeof(unsigned long long)));
+    const unsigned long long none = ~0ull;
+    HIPCHK(c, hipMemcpyAsync(bad.p, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_line_setup(A->d_indptr, A->d_indices, A->d_data, A->fp32, M->line,
+                                bad.as<unsigned long long>(), c->stream));
+    unsigned long long br = none;
+    HIPCHK(c, hipMemcpyAsync(&br, bad.p, sizeof(br), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (br != none) return fail(c, VTK_ERR_SINGULAR, "vtk_linejacobi_create: zero or non-finite line pivot at row " + std::to_string(br));
+    *out = M;
+    M = nullptr;
+    return VTK_OK;
+}
+
+int vtk_linejacobi_factors(vtk_prec *M, double *f, int kind) {
+    if (!M || !f) return VTK_ERR_ARG;
+    vtk_ctx *c = M->A->ctx;
+    if (M->kind != VTK_PREC_LINE) return fail(c, VTK_ERR_STATE, "vtk_linejacobi_factors: not a line-Jacobi preconditioner");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (M->line.n > 0)
+        HIPCHK(c, hipMemcpy(f, M->line.f, 3 * M->line.n * sizeof(double), kind == VTK_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    return VTK_OK;
+}
+
+int vtk_prec_apply(vtk_prec *M, const double *r, double *z, int kind) { return vtk_bjacobi_apply(M, r, z, kind); }
+
+int vtk_prec_kind_of(vtk_prec *M, int *kind) {
+    if (!M || !kind) return VTK_ERR_ARG;
+    *kind = M->kind;
+    return VTK_OK;
+}
+
 int vtk_bjacobi_inverse(vtk_prec *M, double *inv, int kind) {
     if (!M || !inv) return VTK_ERR_ARG;
     vtk_ctx *c = M->A->ctx;
+    if (M->kind != VTK_PREC_BJACOBI) return fail(c, VTK_ERR_STATE, "vtk_bjacobi_inverse: not a block-Jacobi preconditioner");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(inv, M->d_inv, M->nb * M->bs * M->bs * sizeof(double), kind == VTK_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
@@ -1277,7 +1335,7 @@ int vtk_bjacobi_apply(vtk_prec *M, const double *r, double *z, int kind) {
     TRY(stage_in(c, r, n, kind, sr));
     TRY(stage_in(c, kind == VTK_PTR_DEVICE ? z : nullptr, n, kind, sz));
     {
-        Prof pf(c, "bj_apply", -1, 8.0 * M->bs * n + 16.0 * n);
+        Prof pf(c, M->kind == VTK_PREC_LINE ? "line_apply" : "bj_apply", -1, bj_row_bytes(M) * n + 16.0 * n);
         HIPCHK(c, launch_bj_apply(bj_op(M), n, sr.d, sz.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0, c->stream));
     }
     if (c->prof_on) prof_flush(c);
@@ -1322,6 +1380,7 @@ int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out) {
 int vtk_bjacobi_set_mode(vtk_prec *M, int mode) {
     if (!M) return VTK_ERR_ARG;
     vtk_ctx *c = M->A->ctx;
+    if (M->kind != VTK_PREC_BJACOBI) return fail(c, VTK_ERR_STATE, "vtk_bjacobi_set_mode: not a block-Jacobi preconditioner");
     if (mode != VTK_BJ_AUTO && mode != VTK_BJ_INVERSE && mode != VTK_BJ_TRIDIAG)
         return fail(c, VTK_ERR_ARG, "vtk_bjacobi_set_mode: unknown mode");
     if (mode == VTK_BJ_TRIDIAG && !M->tri_ok)
@@ -1332,6 +1391,7 @@ int vtk_bjacobi_set_mode(vtk_prec *M, int mode) {
 
 int vtk_bjacobi_get_mode(vtk_prec *M, int *mode_in_use, int *tridiag_available) {
     if (!M) return VTK_ERR_ARG;
+    if (M->kind != VTK_PREC_BJACOBI) return fail(M->A->ctx, VTK_ERR_STATE, "vtk_bjacobi_get_mode: not a block-Jacobi preconditioner");
     if (mode_in_use) *mode_in_use = bj_op(M).tri ? VTK_BJ_TRIDIAG : VTK_BJ_INVERSE;
     if (tridiag_available) *tridiag_available = M->tri_ok ? 1 : 0;
     return VTK_OK;
@@ -1342,6 +1402,7 @@ void vtk_prec_destroy(vtk_prec *M) {
     if (M->A && M->A->ctx) (void)hipSetDevice(M->A->ctx->device);
     (void)hipFree(M->d_inv);
     (void)hipFree(M->d_tri);
+    (void)hipFree(M->line.f);
     free_tiles(M->tiles);
     free_tiles(M->tiles_in);
     free_tiles(M->tiles_bd);

@@ -90,6 +90,19 @@ struct Groups {
     int grid = 0;               // workgroups = min(count, GMAX), >= 1
 };
 
+// line-Jacobi operator: the tridiagonal systems along x-lines, cut into
+// segments of `seg` consecutive line indices i = R / stride (R global) and at the rank's row
+// block [row0, row0 + n).  f = [l | m | g] (n doubles each), Thomas factors (vtk_kernels.hip
+// k_line_setup; the oracle's orc_line_setup).  Work items: one wavefront per (segment, 64
+// consecutive j = R mod stride starting at j0).
+struct LineOp {
+    double *f = nullptr;
+    int64_t n = 0, row0 = 0, stride = 1, seg = 1;
+    int64_t i_lo = 0, i_hi = -1;   // line indices of the block's first / last row
+    int64_t nseg = 0;              // segments touching the block
+    int64_t j0 = 0, jn = 0;        // lanes cover j = j0 .. j0 + jn - 1
+    int64_t jb = 0;                // wavefronts per segment = ceil(jn / 64)
+};
 }  // namespace vtk
 
 struct vtk_ctx {
@@ -165,6 +178,9 @@ struct vtk_prec {
     int64_t tri_ld = 0;
     bool tri_ok = false;
     int mode = VTK_BJ_AUTO;
+    // line Jacobi (vtk_linejacobi_create): kind VTK_PREC_LINE, factors in line.f
+    int kind = VTK_PREC_BJACOBI;
+    vtk::LineOp line;
 };
 
 namespace vtk {
@@ -181,6 +197,8 @@ struct SpmvIn {
     const Groups *groups = nullptr;
 };
 
+LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);
+
 // block-Jacobi operator as the kernels see it: inverse rows f64[nb][bs][bs], or (tri != null)
 // the LU factors of tridiagonal blocks, SoA l | m | g with stride tri_ld (vtk_api.cpp, BJ
 // modes).  bs == 0: identity.
@@ -189,6 +207,7 @@ struct BjOp {
     const double *tri = nullptr;
     int64_t tri_ld = 0;
     int bs = 0;
+    const LineOp *line = nullptr;   // line Jacobi instead (inv/tri unused)
 };
 
 // workgroups (= partials) of a launch on this input
@@ -221,6 +240,12 @@ size_t sell_scan_bytes(int64_t n);
 hipError_t launch_sell_pack(const int64_t *off, int64_t nch, int64_t *pkoff, int64_t *tmp64, void *scan_tmp,
                             size_t scan_bytes, const int32_t *col, uint32_t *pk, int32_t *dict,
                             unsigned long long *wide_cnt, int phase, hipStream_t s);
+// line Jacobi: factors (flags: *bad_row = min global row with a zero / non-finite pivot) and
+// z = M^-1 r with part0 = sum z^2, part1 = sum v0*z (optional) over `grid` workgroups
+hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
+                             const LineOp &L, unsigned long long *bad_row, hipStream_t s);
+hipError_t launch_line_apply(const LineOp &L, const double *r, double *z, const double *v0, double *part0,
+                             double *part1, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
                                int64_t n, int bs, const double *inv, double *tri, int64_t ld, int *flags,
                                hipStream_t s);

@@ -1002,6 +1002,7 @@ __global__ __launch_bounds__(NT) void k_bj_apply_tri(const double *__restrict__ 
 hipError_t launch_bj_apply(const BjOp &bj, int64_t n, const double *r, double *z,
                            const double *v0, double *part0, double *part1, int grid,
                            const int *stop_col, int col, hipStream_t s) {
+    if (bj.line) return launch_line_apply(*bj.line, r, z, v0, part0, part1, grid, stop_col, col, s);
     if (n == 0 && part0 == nullptr) return hipSuccess;
     if (bj.tri) {
         switch (bj.bs) {
@@ -1094,6 +1095,199 @@ hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, co
     const dim3 g((unsigned)((nb + NT - 1) / NT));
     if (fp32) hipLaunchKernelGGL(k_bj_tri_setup<float>, g, dim3(NT), 0, s, indptr, indices, (const float *)data, n, nb, bs, inv, tri, ld, flags);
     else hipLaunchKernelGGL(k_bj_tri_setup<double>, g, dim3(NT), 0, s, indptr, indices, (const double *)data, n, nb, bs, inv, tri, ld, flags);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// line Jacobi: tridiagonal systems along x-line segments.  One lane per
+// (segment, j); the 64 lanes of a wavefront take consecutive j, so every sweep step over the
+// line index i (row R = i*stride + j) is one coalesced 512-B access per array.  The IEEE
+// operations per row are those of orc_line_setup / orc_line_apply (bit-identical).
+// ------------------------------------------------------------------------------------------
+LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg) {
+    LineOp L;
+    L.n = n;
+    L.row0 = row0;
+    L.stride = stride;
+    L.seg = seg;
+    if (n <= 0 || stride <= 0 || seg <= 0) return L;
+    L.i_lo = row0 / stride;
+    L.i_hi = (row0 + n - 1) / stride;
+    L.nseg = L.i_hi / seg - L.i_lo / seg + 1;
+    if (L.i_lo == L.i_hi) {
+        L.j0 = row0 % stride;
+        L.jn = n;
+    } else {
+        L.j0 = 0;
+        L.jn = stride;
+    }
+    L.jb = (L.jn + 63) / 64;
+    return L;
+}
+
+// wavefront item t -> the segment's line range [i_beg, i_end) and this lane's j (jv: in range)
+struct LineLane {
+    int64_t i_beg, i_end, j;
+    bool jv;
+};
+__device__ __forceinline__ LineLane line_lane(const LineOp &L, int64_t t, int lane) {
+    const int64_t k = t / L.jb, jw = t - k * L.jb;
+    const int64_t s = L.i_lo / L.seg + k;
+    LineLane o;
+    o.i_beg = s * L.seg > L.i_lo ? s * L.seg : L.i_lo;
+    o.i_end = (s + 1) * L.seg < L.i_hi + 1 ? (s + 1) * L.seg : L.i_hi + 1;
+    const int64_t jj = jw * 64 + lane;
+    o.jv = jj < L.jn;
+    o.j = L.j0 + jj;
+    return o;
+}
+
+// Thomas factors along the lane's line segment: u = b | l = a / u_prev, u = b - l c_prev;
+// m = 1 / u; g = c m.  A row's "previous" is the lane's previous valid row (rows of one (j,
+// segment) inside the block are contiguous in i), exactly the oracle's line_has(R, -1).
+template <typename VT>
+__global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ indptr,
+                                                   const int32_t *__restrict__ indices,
+                                                   const VT *__restrict__ data, LineOp L,
+                                                   unsigned long long *bad_row) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 6;
+    if (t >= L.nseg * L.jb) return;
+    const LineLane q = line_lane(L, t, lane);
+    if (!q.jv) return;
+    const int64_t S = L.stride, r_end = L.row0 + L.n;
+    double *l = L.f, *m = L.f + L.n, *g = L.f + 2 * L.n;
+    double up = 0.0, cp = 0.0;
+    bool have = false;
+    for (int64_t i = q.i_beg; i < q.i_end; ++i) {
+        const int64_t R = i * S + q.j;
+        if (R < L.row0 || R >= r_end) continue;
+        const int64_t r = R - L.row0;
+        const bool hl = have, hr = i + 1 < q.i_end && R + S < r_end;
+        double b = 0.0, a = 0.0, c = 0.0;
+        for (int32_t k = indptr[r]; k < indptr[r + 1]; ++k) {
+            const int64_t col = indices[k];
+            const double v = (double)data[k];
+            if (col == r) b += v;
+            else if (hl && col == r - S) a += v;
+            else if (hr && col == r + S) c += v;
+        }
+        double lv = 0.0, uv;
+        if (hl) {
+            lv = a / up;
+            uv = b - lv * cp;
+        } else {
+            uv = b;
+        }
+        const double mv = 1.0 / uv;
+        if (uv == 0.0 || !isfinite(uv) || !isfinite(mv)) atomicMin(bad_row, (unsigned long long)R);
+        l[r] = lv;
+        m[r] = mv;
+        g[r] = c * mv;
+        up = uv;
+        cp = c;
+        have = true;
+    }
+}
+
+// z = M^-1 r: forward d = r - l d_prev, backward z = m d - g z_next.  LMAX > 0: the segment's
+// d stays in registers and every load of a sweep is issued before its recurrence (addresses
+// clamped to row 0 off the block, results discarded); LMAX == 0 (segments longer than 32):
+// d goes through z.  r and z may alias (each row is read before it is written, by its lane).
+template <int LMAX>
+__global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, double *z,
+                                                   const double *__restrict__ v0, double *part0,
+                                                   double *part1, const int *stop_col, int col) {
+    __shared__ double red[NT / 64];
+    if (stopped(stop_col, col)) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nitems = L.nseg * L.jb, S = L.stride, r0 = L.row0, r_end = L.row0 + L.n;
+    const double *l = L.f, *m = L.f + L.n, *g = L.f + 2 * L.n;
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int64_t t = (int64_t)blockIdx.x * (NT / 64) + wv; t < nitems; t += (int64_t)gridDim.x * (NT / 64)) {
+        const LineLane q = line_lane(L, t, lane);
+        const int64_t len = q.i_end - q.i_beg;
+        if constexpr (LMAX > 0) {
+            // row offsets k_u = k0 + u*S fit 32 bits (n_local < 2^31): 32-bit address math
+            const int64_t k0l = q.i_beg * S + q.j - r0;
+            const int nn = (int)L.n;
+            double d[LMAX];
+            double dp = 0.0;
+#pragma unroll
+            for (int u = 0; u < LMAX; ++u) {
+                const int64_t kl = k0l + (int64_t)u * S;
+                const bool ok = q.jv && u < len && kl >= 0 && kl < nn;
+                const int k = ok ? (int)kl : 0;
+                const double dv = r[k] - l[k] * dp;
+                d[u] = dv;
+                dp = ok ? dv : dp;
+            }
+            double zn = 0.0;
+#pragma unroll
+            for (int u = LMAX - 1; u >= 0; --u) {
+                const int64_t kl = k0l + (int64_t)u * S;
+                const bool ok = q.jv && u < len && kl >= 0 && kl < nn;
+                const int k = ok ? (int)kl : 0;
+                const double zv = m[k] * d[u] - g[k] * zn;
+                if (ok) {
+                    z[k] = zv;
+                    zn = zv;
+                    acc0 += zv * zv;
+                    if (v0) acc1 += v0[k] * zv;
+                }
+            }
+        } else {
+            double dp = 0.0;
+            for (int64_t u = 0; u < len; ++u) {
+                const int64_t R = (q.i_beg + u) * S + q.j;
+                if (!q.jv || R < r0 || R >= r_end) continue;
+                const int64_t k = R - r0;
+                const double dv = r[k] - l[k] * dp;
+                z[k] = dv;
+                dp = dv;
+            }
+            double zn = 0.0;
+            for (int64_t u = len - 1; u >= 0; --u) {
+                const int64_t R = (q.i_beg + u) * S + q.j;
+                if (!q.jv || R < r0 || R >= r_end) continue;
+                const int64_t k = R - r0;
+                const double zv = m[k] * z[k] - g[k] * zn;
+                z[k] = zv;
+                zn = zv;
+                acc0 += zv * zv;
+                if (v0) acc1 += v0[k] * zv;
+            }
+        }
+    }
+    if (part0) {
+        const double t0 = block_sum(acc0, red);
+        if (threadIdx.x == 0) part0[blockIdx.x] = t0;
+    }
+    if (part1 && v0) {
+        const double t1 = block_sum(acc1, red);
+        if (threadIdx.x == 0) part1[blockIdx.x] = t1;
+    }
+}
+
+hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
+                             const LineOp &L, unsigned long long *bad_row, hipStream_t s) {
+    const int64_t threads = L.nseg * L.jb * 64;
+    if (threads == 0) return hipSuccess;
+    const dim3 g((unsigned)((threads + NT - 1) / NT));
+    if (fp32) hipLaunchKernelGGL(k_line_setup<float>, g, dim3(NT), 0, s, indptr, indices, (const float *)data, L, bad_row);
+    else hipLaunchKernelGGL(k_line_setup<double>, g, dim3(NT), 0, s, indptr, indices, (const double *)data, L, bad_row);
+    return hipGetLastError();
+}
+
+hipError_t launch_line_apply(const LineOp &L, const double *r, double *z, const double *v0, double *part0,
+                             double *part1, int grid, const int *stop_col, int col, hipStream_t s) {
+    if (L.n == 0 && part0 == nullptr) return hipSuccess;
+    const dim3 g(grid), b(NT);
+    if (L.seg <= 8) hipLaunchKernelGGL(k_line_apply<8>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
+    else if (L.seg <= 16) hipLaunchKernelGGL(k_line_apply<16>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
+    else if (L.seg <= 25) hipLaunchKernelGGL(k_line_apply<25>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
+    else if (L.seg <= 32) hipLaunchKernelGGL(k_line_apply<32>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
+    else hipLaunchKernelGGL(k_line_apply<0>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
     return hipGetLastError();
 }
 

@@ -26,7 +26,8 @@ from ._abi import check, lib
 
 __all__ = ["Context", "default_context", "csr_matrix", "load_npz", "save_npz", "vlasov_operator", "block_jacobi",
            "gmres", "VlasovParams", "vlasov_params", "rhs_splitmix", "partition_rows",
-           "halo_plan", "device_count", "SolveStats"]
+           "halo_plan", "device_count", "SolveStats", "line_jacobi", "LineJacobi",
+           "vlasov_line_stride"]
 
 VlasovParams = _abi.VlasovParams
 
@@ -384,6 +385,78 @@ def block_jacobi(A: CsrOperator, bs: int = 8, mode: str = "auto") -> BlockJacobi
     return BlockJacobi(A, bs, mode)
 
 
+class LineJacobi:
+    """Line-Jacobi preconditioner (line-implicit x-direction solve):
+    M = A's diagonal + the couplings between rows R and R +- ``stride`` within segments of
+    ``seg`` consecutive line indices R // stride (and within this rank's rows).  SciPy
+    statement: ``LinearOperator(matvec=splu(M).solve)``.  ``vtk_linejacobi_create``.
+
+    For the Vlasov operators ``stride`` = 1 (1D), Nv (2D), Ny*Nvx*Nvy (4D): see
+    :func:`vlasov_line_stride`.  Choose ``seg`` dividing Nx / world so that M does not depend
+    on the number of ranks."""
+
+    def __init__(self, A: CsrOperator, stride: int, seg: int = 25):
+        h = C.c_void_p()
+        check(lib().vtk_linejacobi_create(A.handle, int(stride), int(seg), C.byref(h)), A.ctx.handle)
+        self._h = h
+        self.A = A
+        self.stride = int(stride)
+        self.seg = int(seg)
+        self.shape = A.shape
+        self.dtype = np.dtype(np.float64)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def factors(self) -> np.ndarray:
+        """l | m | g, 3 * n_local doubles (the oracle's orc_line_setup layout)."""
+        f = np.empty(3 * self.A.n_local)
+        check(lib().vtk_linejacobi_factors(self._h, _np_ptr(f), _abi.PTR_HOST), self.A.ctx.handle)
+        return f
+
+    def matvec(self, r):
+        vr = _Vec(r, self.A.n_local)
+        if vr.kind == _abi.PTR_DEVICE:
+            import torch
+            z = torch.empty_like(vr.obj)
+            check(lib().vtk_prec_apply(self._h, vr.ptr, C.c_void_p(z.data_ptr()), vr.kind), self.A.ctx.handle)
+            self.A.ctx.synchronize()
+            return z
+        z = np.empty(self.A.n_local)
+        check(lib().vtk_prec_apply(self._h, vr.ptr, _np_ptr(z), vr.kind), self.A.ctx.handle)
+        return z
+
+    def __matmul__(self, r):
+        return self.matvec(r)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vtk_prec_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def line_jacobi(A: CsrOperator, stride: int, seg: int = 25) -> LineJacobi:
+    return LineJacobi(A, stride, seg)
+
+
+def vlasov_line_stride(params) -> int:
+    """Rows between x-neighbours of a Vlasov operator: 1 (1D), Nv (2D), Ny*Nvx*Nvy (4D)."""
+    dim = int(params.dim)
+    sh = [int(v) for v in params.shape]
+    if dim == 1:
+        return 1
+    if dim == 2:
+        return sh[1]
+    return sh[1] * sh[2] * sh[3]
+
+
 @dataclass
 class SolveStats:
     inner_iters: int
@@ -410,8 +483,8 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     """``scipy.sparse.linalg.gmres`` on the GPU (iterative.py:582-841, left-preconditioned
     restarted GMRES with modified Gram-Schmidt).  Returns ``(x, info)``.
 
-    ``A``: a :class:`CsrOperator` or any SciPy sparse matrix (uploaded).  ``M``: None or a
-    :class:`BlockJacobi` built on ``A``; any other preconditioner raises TypeError (no CPU
+    ``A``: a :class:`CsrOperator` or any SciPy sparse matrix (uploaded).  ``M``: None, a
+    :class:`BlockJacobi` or a :class:`LineJacobi` built on ``A``; any other preconditioner raises TypeError (no CPU
     fallback).  ``callback`` is not supported (the Arnoldi loop never returns to the host).
     ``orth`` (extension): "mgs" (SciPy's exact sequence), "dcgs2" (one reduction per step,
     restart <= 32) or "auto"/None (the context's setting; default DCGS2 when restart <= 32).
@@ -420,8 +493,8 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     if callback is not None:
         raise NotImplementedError("vtkrylov.gmres: callbacks would force a host round trip per "
                                   "Arnoldi step and are not supported")
-    if M is not None and not isinstance(M, BlockJacobi):
-        raise TypeError("vtkrylov.gmres: M must be None or vtkrylov.BlockJacobi")
+    if M is not None and not isinstance(M, (BlockJacobi, LineJacobi)):
+        raise TypeError("vtkrylov.gmres: M must be None, vtkrylov.BlockJacobi or vtkrylov.LineJacobi")
     if not isinstance(A, CsrOperator):
         A = csr_matrix(A)
     if atol == "legacy" or atol is None or atol < 0:

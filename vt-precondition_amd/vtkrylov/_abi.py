@@ -86,6 +86,10 @@ PROTOTYPES = {
     "vtk_csr_layout_info": (C.c_int, [P, C.c_void_p]),
     "vtk_bjacobi_get_mode": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_destroy": (None, [P]),
+    "vtk_linejacobi_create": (C.c_int, [P, C.c_int64, C.c_int64, C.POINTER(P)]),
+    "vtk_linejacobi_factors": (C.c_int, [P, P, C.c_int]),
+    "vtk_prec_apply": (C.c_int, [P, P, P, C.c_int]),
+    "vtk_prec_kind_of": (C.c_int, [P, C.POINTER(C.c_int)]),
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
                             C.POINTER(C.c_int), C.POINTER(Stats)]),
     "vtk_gmres_set_orth": (C.c_int, [P, C.c_int]),
