@@ -25,7 +25,7 @@ def _free_port():
 class DistOps:
     """Distributed SpMV / BJ / dot of one rank, mirroring vtk_api.cpp's multi-rank schedule."""
 
-    def __init__(self, vk, dist, p, offs, rank, world):
+    def __init__(self, vk, dist, p, offs, rank, world, prec="bj", seg=0):
         from oracle import coracle
         self.dist, self.rank, self.world = dist, rank, world
         self.rb, self.re = int(offs[rank]), int(offs[rank + 1])
@@ -46,6 +46,11 @@ class DistOps:
         self.send_idx = got.numpy() - self.rb
         assert np.all((self.send_idx >= 0) & (self.send_idx < self.re - self.rb))
         self.inv = coracle.bj_setup(ip, self.loc, d, 8)   # blocks never reach halo columns
+        # line Jacobi: rank-local lines (vtk_linejacobi_create cuts segments at the row block)
+        self.lf = None
+        if prec == "line":
+            stride = 1 if p.dim == 1 else (p.shape[1] if p.dim == 2 else p.n // p.shape[0])
+            self.lf = coracle.line_setup(ip, ix, d, stride, seg, row0=self.rb)
 
     def halo(self, xl):
         import torch
@@ -60,6 +65,8 @@ class DistOps:
 
     def psolve(self, r):
         from oracle import coracle
+        if self.lf is not None:
+            return coracle.line_apply(self.lf, r)
         return coracle.bj_apply(self.inv, r)
 
     def dot(self, a, b):
@@ -139,7 +146,7 @@ def dist_gmres(ops, b, rtol, restart=20, maxiter=1000):
     return x, (0 if rnorm <= atol else maxiter), inner
 
 
-def _worker(rank, world, port, case, outdir):
+def _worker(rank, world, port, case, outdir, prec="bj", seg=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -149,7 +156,7 @@ def _worker(rank, world, port, case, outdir):
     p = twin.CONFIGS[case]
     align = p.shape[-1] if p.dim == 2 else (8 if p.dim == 1 else p.shape[-1] * p.shape[-2])
     offs = vk.partition_rows(p.n, world, align)
-    ops = DistOps(vk, dist, p, offs, rank, world)
+    ops = DistOps(vk, dist, p, offs, rank, world, prec, seg)
     b = twin.rhs(p.n)[ops.rb:ops.re]
     x, info, inner = dist_gmres(ops, b, 1e-8)
     # the host-staged communicator hooks, called the way the library calls them
@@ -192,6 +199,27 @@ def test_distributed_gmres_matches_single_rank(tmp_path, case, world):
     for r in range(world):
         z = np.load(tmp_path / f"rank{r}.npz")
         assert int(z["halo"]) > 0
+        assert int(z["info"]) == ref.info == 0
+        assert abs(int(z["inner"]) - ref.inner_iters) <= 1
+        x[int(z["rb"]):int(z["re"])] = z["x"]
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) <= 1e-10
+
+
+@pytest.mark.parametrize("case,world,seg", [("S2", 2, 8), ("S4", 2, 3)])
+def test_distributed_line_jacobi_matches_single_rank(tmp_path, case, world, seg):
+    """Line Jacobi with segments that divide every rank's x-range: the rank-local M equals the
+    single-rank M, so the distributed solve reproduces the single-rank oracle."""
+    import torch.multiprocessing as mp
+
+    from oracle import coracle, twin
+    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), "line", seg), nprocs=world, join=True)
+    p = twin.CONFIGS[case]
+    ip, ix, d = coracle.generate(p)
+    stride = p.shape[1] if p.dim == 2 else p.n // p.shape[0]
+    ref = coracle.gmres(ip, ix, d, twin.rhs(p.n), coracle.line_setup(ip, ix, d, stride, seg), rtol=1e-8)
+    x = np.zeros(p.n)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
         assert int(z["info"]) == ref.info == 0
         assert abs(int(z["inner"]) - ref.inner_iters) <= 1
         x[int(z["rb"]):int(z["re"])] = z["x"]

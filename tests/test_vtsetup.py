@@ -23,6 +23,10 @@ def test_typed_config_and_overrides():
     assert (c.config, c.dim, c.shape, c.fp32) == ("C3", 2, (25000, 800), False)
     assert (c.rtol, c.atol, c.restart, c.block_size, c.seed) == (1e-8, 0.0, 20, 8, 0x5EED)
     assert (c.orth, c.operator_file) == ("auto", "")
+    assert (c.preconditioner, c.line_stride, c.line_segment) == ("block_jacobi", 0, 25)
+    assert SolverConfig.load(preconditioner="line_jacobi").preconditioner == "line_jacobi"
+    with pytest.raises(ValueError):
+        SolverConfig.load(preconditioner="ilu")
     c4 = SolverConfig.load(config="C4")
     assert (c4.dim, c4.shape, c4.fp32) == (4, (200, 125, 50, 40), True)
     assert parse_config_spec("1:10000:f64") == (1, (10000,), False)
@@ -73,3 +77,21 @@ def test_step_main_solves_npz_archive(gpu, tmp_path):
     assert res["solve"]["info"] == 0 and res["operator"]["source"] == str(f)
     ref = coracle.gmres(ip, ix, d, twin.rhs(p.n), coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
     assert abs(res["solve"]["inner_iters"] - ref.inner_iters) <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["S2", "C1"])
+def test_step_main_line_jacobi(gpu, tmp_path, name):
+    """preconditioner/type = line_jacobi: stride from the Vlasov config, SciPy-pinned oracle."""
+    from oracle import coracle, twin
+    from vtsetup.krylov_precondition import KrylovPrecondition
+    cfg = SolverConfig.load(config=name, report=str(tmp_path / "r.json"), preconditioner="line_jacobi")
+    step = KrylovPrecondition(cfg, ctx=gpu)
+    res = step.main()
+    p = twin.CONFIGS[name]
+    assert res["solve"]["info"] == 0 and res["preconditioner"]["line_stride"] == p.shape[1]
+    ip, ix, d = coracle.generate(p)
+    b = twin.rhs(p.n)
+    ref = coracle.gmres(ip, ix, d, b, coracle.line_setup(ip, ix, d, p.shape[1], 25), rtol=1e-8)
+    assert abs(res["solve"]["inner_iters"] - ref.inner_iters) <= 1
+    assert np.linalg.norm(b - coracle.spmv(ip, ix, d, step.x)) <= 1e-8 * np.linalg.norm(b)

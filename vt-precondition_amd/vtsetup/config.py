@@ -62,6 +62,8 @@ class SolverConfig:
     operator_file: str
     preconditioner: str
     block_size: int
+    line_stride: int
+    line_segment: int
     seed: int
     device: int
     report: str
@@ -84,13 +86,15 @@ class SolverConfig:
                   operator_file=t.get_node_value("operator/file"),
                   preconditioner=t.get_node_value("preconditioner/type").lower(),
                   block_size=int(t.get_node_value("preconditioner/block_size")),
+                  line_stride=int(t.get_node_value("preconditioner/line_stride")),
+                  line_segment=int(t.get_node_value("preconditioner/line_segment")),
                   seed=int(t.get_node_value("rhs/seed"), 0),
                   device=int(t.get_node_value("run/device")),
                   report=t.get_node_value("run/report"))
         for k, v in overrides.items():
             if v is not None:
                 setattr(cfg, k, v)
-        if cfg.preconditioner not in ("block_jacobi", "none"):
+        if cfg.preconditioner not in ("block_jacobi", "line_jacobi", "none"):
             raise ValueError(f"unknown preconditioner {cfg.preconditioner!r}")
         if cfg.orth not in ("auto", "mgs", "dcgs2"):
             raise ValueError(f"unknown orthogonalisation {cfg.orth!r}")

@@ -43,11 +43,21 @@ class KrylovPrecondition:
     def setup_preconditioner(self):
         import vtkrylov as vk
         t = time.perf_counter()
-        if self.cfg.preconditioner == "block_jacobi":
-            self.M = vk.block_jacobi(self.A, self.cfg.block_size)
-        self.result["preconditioner"] = {"type": self.cfg.preconditioner,
-                                         "block_size": self.cfg.block_size,
-                                         "t_setup_s": time.perf_counter() - t}
+        c = self.cfg
+        info = {"type": c.preconditioner}
+        if c.preconditioner == "block_jacobi":
+            self.M = vk.block_jacobi(self.A, c.block_size)
+            info["block_size"] = c.block_size
+        elif c.preconditioner == "line_jacobi":
+            stride = c.line_stride
+            if stride <= 0:
+                if c.operator_file:
+                    raise ValueError("line_jacobi on an operator file needs preconditioner/line_stride")
+                stride = vk.vlasov_line_stride(vk.vlasov_params(c.dim, c.shape))
+            self.M = vk.line_jacobi(self.A, stride, c.line_segment)
+            info.update(line_stride=stride, line_segment=c.line_segment)
+        info["t_setup_s"] = time.perf_counter() - t
+        self.result["preconditioner"] = info
 
     def solve(self):
         import vtkrylov as vk
@@ -82,9 +92,11 @@ def test_main(argv=None) -> int:
     ap.add_argument("--config")
     ap.add_argument("--report")
     ap.add_argument("--operator-file", help="SciPy save_npz CSR archive to solve")
+    ap.add_argument("--preconditioner", choices=["block_jacobi", "line_jacobi", "none"])
     a = ap.parse_args(argv)
     try:
-        cfg = SolverConfig.load(a.xml, config=a.config, report=a.report, operator_file=a.operator_file)
+        cfg = SolverConfig.load(a.xml, config=a.config, report=a.report, operator_file=a.operator_file,
+                                 preconditioner=a.preconditioner)
         res = KrylovPrecondition(cfg).main()
         print(json.dumps(res))
         return 0 if res["solve"]["info"] == 0 else 1
