@@ -353,7 +353,7 @@ def line_factors_numpy(indptr, indices, data, n, stride, seg, row0=0):
             k = np.arange(lo, hi)
             first = ~hl[k]
             kp = np.where(first, k, k - stride)
-            lv = np.where(first, 0.0, a[k] / u[kp])
+            lv = np.where(first, 0.0, a[k] * m[kp])
             uv = np.where(first, b[k], b[k] - lv * np.where(first, 0.0, c[kp]))
             u[k] = uv
             l[k] = lv

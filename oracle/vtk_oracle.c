@@ -258,10 +258,12 @@ void orc_lartg(double f, double g, double *c, double *s, double *r) {
  * index i = R / stride falls in the same segment i / seg, both rows inside [row0, row0 + n).
  * Each (segment, j = R mod stride) is a tridiagonal system along its line; Thomas without
  * pivoting over the line in ascending i:
- *   u = b (first row) | l = a / u_prev, u = b - l * c_prev;   m = 1 / u;   g = c * m
+ *   u = b (first row) | l = a * m_prev, u = b - l * c_prev;   m = 1 / u;   g = c * m
  * with b, a, c the sums (stored order, from 0.0: toarray() semantics) of the row's entries in
  * columns R, R - stride, R + stride.  f = [l | m | g], n doubles each (l = 0 on first rows).
- * The HIP setup (vtk_kernels.hip k_line_setup) runs the same IEEE operations per line. */
+ * (l = a * m_prev rather than a / u_prev: the fused SpMV + line kernel forms l from the row's own
+ * entry a and the previous row's m, so only m is stored for it.)  The HIP setup
+ * (vtk_kernels.hip k_line_setup) runs the same IEEE operations per line. */
 static int line_has(int64_t R, int64_t d, int64_t row0, int64_t n, int64_t stride, int64_t seg) {
     const int64_t Q = R + d * stride;
     return Q >= row0 && Q < row0 + n && (Q / stride) / seg == (R / stride) / seg;
@@ -285,7 +287,7 @@ int64_t orc_line_setup(int64_t n, const int32_t *indptr, const int32_t *indices,
         }
         double lv = 0.0, uv;
         if (hl) {
-            lv = a / u[r - stride];
+            lv = a * mm[r - stride];
             uv = b - lv * cs[r - stride];
         } else {
             uv = b;

@@ -21,9 +21,9 @@ def pytest_configure(config):
 
 
 def pytest_sessionstart(session):
-    # the CPU oracle is test infrastructure: build it if needed (gcc, seconds)
-    if not os.path.exists(os.path.join(ROOT, "oracle", "lib", "libvtk_oracle.so")):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    # the CPU oracle is test infrastructure: (re)build it when missing or older than its
+    # sources (make, gcc: seconds)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
 
 
 @pytest.fixture(scope="session")

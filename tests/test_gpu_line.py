@@ -239,3 +239,4 @@ def test_line_ranks_sharing_one_gpu(tmp_path, case, world, orth):
         z0 = np.load(tmp_path / "rank0.npz", allow_pickle=False)
         assert abs(int(z0["iters"]) - ref.inner_iters) <= 1
         assert np.linalg.norm(xs - ref.x) / np.linalg.norm(ref.x) <= 1e-9
+

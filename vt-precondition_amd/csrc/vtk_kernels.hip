@@ -1142,7 +1142,7 @@ __device__ __forceinline__ LineLane line_lane(const LineOp &L, int64_t t, int la
     return o;
 }
 
-// Thomas factors along the lane's line segment: u = b | l = a / u_prev, u = b - l c_prev;
+// Thomas factors along the lane's line segment: u = b | l = a m_prev, u = b - l c_prev;
 // m = 1 / u; g = c m.  A row's "previous" is the lane's previous valid row (rows of one (j,
 // segment) inside the block are contiguous in i), exactly the oracle's line_has(R, -1).
 template <typename VT>
@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ i
     if (!q.jv) return;
     const int64_t S = L.stride, r_end = L.row0 + L.n;
     double *l = L.f, *m = L.f + L.n, *g = L.f + 2 * L.n;
-    double up = 0.0, cp = 0.0;
+    double mp = 0.0, cp = 0.0;
     bool have = false;
     for (int64_t i = q.i_beg; i < q.i_end; ++i) {
         const int64_t R = i * S + q.j;
@@ -1174,7 +1174,7 @@ __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ i
         }
         double lv = 0.0, uv;
         if (hl) {
-            lv = a / up;
+            lv = a * mp;
             uv = b - lv * cp;
         } else {
             uv = b;
@@ -1184,7 +1184,7 @@ __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ i
         l[r] = lv;
         m[r] = mv;
         g[r] = c * mv;
-        up = uv;
+        mp = mv;
         cp = c;
         have = true;
     }
