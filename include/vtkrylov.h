@@ -214,6 +214,12 @@ typedef enum { VTK_PREC_BJACOBI = 0, VTK_PREC_LINE = 1 } vtk_prec_kind;
 int vtk_linejacobi_create(vtk_csr *A, int64_t stride, int64_t seg, vtk_prec **out);
 /* export the factors l | m | g (3 * n_local doubles; the oracle's orc_line_setup layout) */
 int vtk_linejacobi_factors(vtk_prec *M, double *f, int ptr_kind);
+/* COMPACT apply (default when available): when every line's x-couplings are bit-equal along
+ * the line (x-invariant advection, as in the Vlasov operators, checked at setup) the apply
+ * forms l and g from them and reads only m: 16 B/row instead of 32, same result bits.
+ * set_compact(0) forces the stored-factor apply; set_compact(1) fails when unavailable. */
+int vtk_linejacobi_set_compact(vtk_prec *M, int on);
+int vtk_linejacobi_get_compact(vtk_prec *M, int *in_use, int *available);
 /* z = M^-1 r for any preconditioner; *kind = vtk_prec_kind */
 int vtk_prec_apply(vtk_prec *M, const double *r, double *z, int ptr_kind);
 int vtk_prec_kind_of(vtk_prec *M, int *kind);

@@ -240,3 +240,32 @@ def test_line_ranks_sharing_one_gpu(tmp_path, case, world, orth):
         assert abs(int(z0["iters"]) - ref.inner_iters) <= 1
         assert np.linalg.norm(xs - ref.x) / np.linalg.norm(ref.x) <= 1e-9
 
+
+
+@pytest.mark.parametrize("name", SMALL + ["C1"])
+def test_compact_apply_bitexact_vs_stored_factors(ops, vk_lib, name):
+    """The Vlasov operators' x-couplings are constant along each line: the compact apply (l, g
+    formed from a_j, c_j and m) must give the stored-factor apply's bits, in GMRES too."""
+    vk = vk_lib
+    p, A, _ = ops[name]
+    M = vk.line_jacobi(A, stride_of(p), SEG)
+    assert M.compact_available and M.compact
+    r = twin.rhs(p.n)
+    zc = M @ r
+    b = twin.rhs(p.n)
+    xc, ic = vk.gmres(A, b, rtol=1e-8, M=M)
+    M.set_compact(False)
+    assert not M.compact
+    assert np.array_equal(bits(zc), bits(M @ r))
+    xg, ig = vk.gmres(A, b, rtol=1e-8, M=M)
+    assert ic == ig == 0 and np.array_equal(bits(xc), bits(xg))
+
+
+def test_compact_unavailable_on_general_csr(gpu, vk_lib, golden):
+    vk = vk_lib
+    ip, ix, d = golden["ragged/indptr"], golden["ragged/indices"], golden["ragged/data"]
+    n = ip.shape[0] - 1
+    M = vk.line_jacobi(vk.csr_matrix((d, ix, ip), shape=(n, n), ctx=gpu), 37, 5)
+    assert not M.compact_available and not M.compact
+    with pytest.raises(ValueError):
+        M.set_compact(True)

@@ -145,7 +145,7 @@ const char *prec_cls(const vtk_prec *M) { return M && M->kind == VTK_PREC_LINE ?
 // algorithmic bytes per row of one BJ application (tridiagonal: the SELL kernels read only m)
 double bj_row_bytes(const vtk_prec *M) {
     if (!M) return 0.0;
-    if (M->kind == VTK_PREC_LINE) return 24.0;   // l, m, g
+    if (M->kind == VTK_PREC_LINE) return M->line.compact ? 8.0 : 24.0;   // m (compact) or l, m, g
     if (bj_op(M).tri) return M->A->use_sell ? 8.0 : 24.0;
     return 8.0 * M->bs;
 }
@@ -1282,16 +1282,42 @@ int vtk_linejacobi_create(vtk_csr *A, int64_t stride, int64_t seg, vtk_prec **ou
     M->bs = 0;
     M->line = line_plan(A->n_local, A->row_begin, stride, seg);
     HIPCHK(c, hipMalloc(&M->line.f, 3 * std::max<int64_t>(A->n_local, 1) * sizeof(double)));
-    DBuf bad;
+    DBuf bad, ext;
+    const int64_t jn = M->line.jn;
     TRY(dalloc(c, bad, sizeof(unsigned long long)));
+    TRY(dalloc(c, ext, 4 * std::max<int64_t>(jn, 1) * sizeof(unsigned long long)));
     const unsigned long long none = ~0ull;
+    std::vector<unsigned long long> hx(4 * (size_t)jn);
+    for (int64_t j = 0; j < jn; ++j) {   // min | max | min | max
+        hx[j] = none; hx[jn + j] = 0; hx[2 * jn + j] = none; hx[3 * jn + j] = 0;
+    }
     HIPCHK(c, hipMemcpyAsync(bad.p, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+    if (jn) HIPCHK(c, hipMemcpyAsync(ext.p, hx.data(), hx.size() * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, launch_line_setup(A->d_indptr, A->d_indices, A->d_data, A->fp32, M->line,
-                                bad.as<unsigned long long>(), c->stream));
+                                bad.as<unsigned long long>(), ext.as<unsigned long long>(), c->stream));
     unsigned long long br = none;
     HIPCHK(c, hipMemcpyAsync(&br, bad.p, sizeof(br), hipMemcpyDeviceToHost, c->stream));
+    if (jn) HIPCHK(c, hipMemcpyAsync(hx.data(), ext.p, hx.size() * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (br != none) return fail(c, VTK_ERR_SINGULAR, "vtk_linejacobi_create: zero or non-finite line pivot at row " + std::to_string(br));
+    // x-invariant couplings (every line's a's bit-equal, likewise its c's): the apply forms l and
+    // g from a_j, c_j and m (16 B/row read instead of 32); lines without any a (c) take 0
+    bool inv = jn > 0;
+    std::vector<double> ac(2 * (size_t)std::max<int64_t>(jn, 1), 0.0);
+    for (int64_t j = 0; j < jn && inv; ++j) {
+        for (int w = 0; w < 2; ++w) {
+            const unsigned long long lo = hx[2 * w * jn + j], hi = hx[(2 * w + 1) * jn + j];
+            if (lo > hi) continue;   // no row of this line has the coupling
+            if (lo != hi) { inv = false; break; }
+            std::memcpy(&ac[w * jn + j], &lo, 8);
+        }
+    }
+    if (inv) {
+        HIPCHK(c, hipMalloc(&M->line.ac, ac.size() * sizeof(double)));
+        HIPCHK(c, hipMemcpy(M->line.ac, ac.data(), ac.size() * sizeof(double), hipMemcpyHostToDevice));
+        M->line.compact = 1;
+    }
+    M->line_compact_ok = inv;
     *out = M;
     M = nullptr;
     return VTK_OK;
@@ -1305,6 +1331,23 @@ int vtk_linejacobi_factors(vtk_prec *M, double *f, int kind) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (M->line.n > 0)
         HIPCHK(c, hipMemcpy(f, M->line.f, 3 * M->line.n * sizeof(double), kind == VTK_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    return VTK_OK;
+}
+
+int vtk_linejacobi_set_compact(vtk_prec *M, int on) {
+    if (!M) return VTK_ERR_ARG;
+    vtk_ctx *c = M->A->ctx;
+    if (M->kind != VTK_PREC_LINE) return fail(c, VTK_ERR_STATE, "vtk_linejacobi_set_compact: not a line-Jacobi preconditioner");
+    if (on && !M->line_compact_ok) return fail(c, VTK_ERR_ARG, "vtk_linejacobi_set_compact: the x-couplings are not constant along the lines");
+    M->line.compact = on ? 1 : 0;
+    return VTK_OK;
+}
+
+int vtk_linejacobi_get_compact(vtk_prec *M, int *in_use, int *available) {
+    if (!M) return VTK_ERR_ARG;
+    if (M->kind != VTK_PREC_LINE) return fail(M->A->ctx, VTK_ERR_STATE, "vtk_linejacobi_get_compact: not a line-Jacobi preconditioner");
+    if (in_use) *in_use = M->line.compact;
+    if (available) *available = M->line_compact_ok ? 1 : 0;
     return VTK_OK;
 }
 
@@ -1403,6 +1446,7 @@ void vtk_prec_destroy(vtk_prec *M) {
     (void)hipFree(M->d_inv);
     (void)hipFree(M->d_tri);
     (void)hipFree(M->line.f);
+    (void)hipFree(M->line.ac);
     free_tiles(M->tiles);
     free_tiles(M->tiles_in);
     free_tiles(M->tiles_bd);

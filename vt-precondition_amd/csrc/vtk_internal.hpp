@@ -102,6 +102,10 @@ struct LineOp {
     int64_t nseg = 0;              // segments touching the block
     int64_t j0 = 0, jn = 0;        // lanes cover j = j0 .. j0 + jn - 1
     int64_t jb = 0;                // wavefronts per segment = ceil(jn / 64)
+    // compact (x-invariant couplings): a_j = ac[j - j0], c_j = ac[jn + j - j0]; the apply forms
+    // l = a m_prev and g = c m and reads only m of f (k_line_setup's ext check)
+    double *ac = nullptr;
+    int compact = 0;
 };
 }  // namespace vtk
 
@@ -181,6 +185,7 @@ struct vtk_prec {
     // line Jacobi (vtk_linejacobi_create): kind VTK_PREC_LINE, factors in line.f
     int kind = VTK_PREC_BJACOBI;
     vtk::LineOp line;
+    bool line_compact_ok = false;   // x-invariant couplings found at setup (line.ac valid)
 };
 
 namespace vtk {
@@ -240,10 +245,11 @@ size_t sell_scan_bytes(int64_t n);
 hipError_t launch_sell_pack(const int64_t *off, int64_t nch, int64_t *pkoff, int64_t *tmp64, void *scan_tmp,
                             size_t scan_bytes, const int32_t *col, uint32_t *pk, int32_t *dict,
                             unsigned long long *wide_cnt, int phase, hipStream_t s);
-// line Jacobi: factors (flags: *bad_row = min global row with a zero / non-finite pivot) and
+// line Jacobi: factors (flags: *bad_row = min global row with a zero / non-finite pivot; ext:
+// 4 jn words, per line min/max bit patterns of the a's and c's, init ~0 / 0 / ~0 / 0) and
 // z = M^-1 r with part0 = sum z^2, part1 = sum v0*z (optional) over `grid` workgroups
 hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
-                             const LineOp &L, unsigned long long *bad_row, hipStream_t s);
+                             const LineOp &L, unsigned long long *bad_row, unsigned long long *ext, hipStream_t s);
 hipError_t launch_line_apply(const LineOp &L, const double *r, double *z, const double *v0, double *part0,
                              double *part1, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,

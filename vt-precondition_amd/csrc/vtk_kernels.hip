@@ -1145,11 +1145,15 @@ __device__ __forceinline__ LineLane line_lane(const LineOp &L, int64_t t, int la
 // Thomas factors along the lane's line segment: u = b | l = a m_prev, u = b - l c_prev;
 // m = 1 / u; g = c m.  A row's "previous" is the lane's previous valid row (rows of one (j,
 // segment) inside the block are contiguous in i), exactly the oracle's line_has(R, -1).
+// ext (4 jn words, lane j - j0): min / max bit pattern of the a's and of the c's the lane's
+// segment holds; equal min and max for every line = the x-couplings are constant along every
+// line (x-invariant advection, the Vlasov operators), and the apply can form l and g from
+// them instead of reading them (LineOp::compact).
 template <typename VT>
 __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ indptr,
                                                    const int32_t *__restrict__ indices,
                                                    const VT *__restrict__ data, LineOp L,
-                                                   unsigned long long *bad_row) {
+                                                   unsigned long long *bad_row, unsigned long long *ext) {
     const int lane = threadIdx.x & 63;
     const int64_t t = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 6;
     if (t >= L.nseg * L.jb) return;
@@ -1159,6 +1163,7 @@ __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ i
     double *l = L.f, *m = L.f + L.n, *g = L.f + 2 * L.n;
     double mp = 0.0, cp = 0.0;
     bool have = false;
+    unsigned long long amin = ~0ull, amax = 0, cmin = ~0ull, cmax = 0;
     for (int64_t i = q.i_beg; i < q.i_end; ++i) {
         const int64_t R = i * S + q.j;
         if (R < L.row0 || R >= r_end) continue;
@@ -1187,14 +1192,36 @@ __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ i
         mp = mv;
         cp = c;
         have = true;
+        if (hl) {
+            const unsigned long long ab = (unsigned long long)__double_as_longlong(a);
+            amin = ab < amin ? ab : amin;
+            amax = ab > amax ? ab : amax;
+        }
+        if (hr) {
+            const unsigned long long cb = (unsigned long long)__double_as_longlong(c);
+            cmin = cb < cmin ? cb : cmin;
+            cmax = cb > cmax ? cb : cmax;
+        }
+    }
+    const int64_t jl = q.j - L.j0;
+    if (amin <= amax) {
+        atomicMin(ext + jl, amin);
+        atomicMax(ext + L.jn + jl, amax);
+    }
+    if (cmin <= cmax) {
+        atomicMin(ext + 2 * L.jn + jl, cmin);
+        atomicMax(ext + 3 * L.jn + jl, cmax);
     }
 }
 
-// z = M^-1 r: forward d = r - l d_prev, backward z = m d - g z_next.  LMAX > 0: the segment's
-// d stays in registers and every load of a sweep is issued before its recurrence (addresses
-// clamped to row 0 off the block, results discarded); LMAX == 0 (segments longer than 32):
-// d goes through z.  r and z may alias (each row is read before it is written, by its lane).
-template <int LMAX>
+// z = M^-1 r: forward d = r - l d_prev, backward z = m d - g z_next.  LMAX > 0: the forward
+// sweep keeps e = m d and g in registers and every load of the sweep is issued before its
+// recurrence (addresses clamped to row 0 off the block, results discarded); the backward
+// sweep only stores.  COMPACT: l = a m_prev and g = c m from the line's constant couplings
+// (L.ac) - 16 B/row read instead of 32; the same IEEE operations as the stored factors.
+// LMAX == 0 (segments longer than 32): d goes through z.  r and z may alias (each row is read
+// before it is written, by its lane).
+template <int LMAX, bool COMPACT>
 __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, double *z,
                                                    const double *__restrict__ v0, double *part0,
                                                    double *part1, const int *stop_col, int col) {
@@ -1211,25 +1238,49 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
             // row offsets k_u = k0 + u*S fit 32 bits (n_local < 2^31): 32-bit address math
             const int64_t k0l = q.i_beg * S + q.j - r0;
             const int nn = (int)L.n;
-            double d[LMAX];
-            double dp = 0.0;
+            double aj = 0.0, cj = 0.0;
+            if constexpr (COMPACT) {
+                if (q.jv) {
+                    aj = L.ac[q.j - L.j0];
+                    cj = L.ac[L.jn + q.j - L.j0];
+                }
+            }
+            double e[LMAX], gg[LMAX];
+            double dp = 0.0, mp = 0.0;
+            bool pok = false;
+            unsigned okm = 0;
 #pragma unroll
             for (int u = 0; u < LMAX; ++u) {
                 const int64_t kl = k0l + (int64_t)u * S;
                 const bool ok = q.jv && u < len && kl >= 0 && kl < nn;
                 const int k = ok ? (int)kl : 0;
-                const double dv = r[k] - l[k] * dp;
-                d[u] = dv;
-                dp = ok ? dv : dp;
+                const double mv = m[k];
+                double lv, gv;
+                if constexpr (COMPACT) {
+                    const bool hl = ok && pok;
+                    const bool hr = ok && u + 1 < len && kl + S < nn;
+                    lv = hl ? aj * mp : 0.0;
+                    gv = (hr ? cj : 0.0) * mv;
+                } else {
+                    lv = l[k];
+                    gv = g[k];
+                }
+                const double dv = r[k] - lv * dp;
+                e[u] = mv * dv;
+                gg[u] = gv;
+                if (ok) {
+                    dp = dv;
+                    mp = mv;
+                }
+                pok = ok;
+                okm |= (unsigned)ok << u;
             }
             double zn = 0.0;
 #pragma unroll
             for (int u = LMAX - 1; u >= 0; --u) {
-                const int64_t kl = k0l + (int64_t)u * S;
-                const bool ok = q.jv && u < len && kl >= 0 && kl < nn;
-                const int k = ok ? (int)kl : 0;
-                const double zv = m[k] * d[u] - g[k] * zn;
-                if (ok) {
+                const double zv = e[u] - gg[u] * zn;
+                if ((okm >> u) & 1u) {
+                    const int k = (int)(k0l + (int64_t)u * S);
                     z[k] = zv;
                     zn = zv;
                     acc0 += zv * zv;
@@ -1270,12 +1321,12 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
 }
 
 hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
-                             const LineOp &L, unsigned long long *bad_row, hipStream_t s) {
+                             const LineOp &L, unsigned long long *bad_row, unsigned long long *ext, hipStream_t s) {
     const int64_t threads = L.nseg * L.jb * 64;
     if (threads == 0) return hipSuccess;
     const dim3 g((unsigned)((threads + NT - 1) / NT));
-    if (fp32) hipLaunchKernelGGL(k_line_setup<float>, g, dim3(NT), 0, s, indptr, indices, (const float *)data, L, bad_row);
-    else hipLaunchKernelGGL(k_line_setup<double>, g, dim3(NT), 0, s, indptr, indices, (const double *)data, L, bad_row);
+    if (fp32) hipLaunchKernelGGL(k_line_setup<float>, g, dim3(NT), 0, s, indptr, indices, (const float *)data, L, bad_row, ext);
+    else hipLaunchKernelGGL(k_line_setup<double>, g, dim3(NT), 0, s, indptr, indices, (const double *)data, L, bad_row, ext);
     return hipGetLastError();
 }
 
@@ -1283,11 +1334,17 @@ hipError_t launch_line_apply(const LineOp &L, const double *r, double *z, const 
                              double *part1, int grid, const int *stop_col, int col, hipStream_t s) {
     if (L.n == 0 && part0 == nullptr) return hipSuccess;
     const dim3 g(grid), b(NT);
-    if (L.seg <= 8) hipLaunchKernelGGL(k_line_apply<8>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
-    else if (L.seg <= 16) hipLaunchKernelGGL(k_line_apply<16>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
-    else if (L.seg <= 25) hipLaunchKernelGGL(k_line_apply<25>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
-    else if (L.seg <= 32) hipLaunchKernelGGL(k_line_apply<32>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
-    else hipLaunchKernelGGL(k_line_apply<0>, g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
+#define VTK_LINE_LAUNCH(LM)                                                                                  \
+    do {                                                                                                     \
+        if (L.compact) hipLaunchKernelGGL((k_line_apply<LM, true>), g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col); \
+        else hipLaunchKernelGGL((k_line_apply<LM, false>), g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);        \
+    } while (0)
+    if (L.seg <= 8) VTK_LINE_LAUNCH(8);
+    else if (L.seg <= 16) VTK_LINE_LAUNCH(16);
+    else if (L.seg <= 25) VTK_LINE_LAUNCH(25);
+    else if (L.seg <= 32) VTK_LINE_LAUNCH(32);
+    else hipLaunchKernelGGL((k_line_apply<0, false>), g, b, 0, s, L, r, z, v0, part0, part1, stop_col, col);
+#undef VTK_LINE_LAUNCH
     return hipGetLastError();
 }
 

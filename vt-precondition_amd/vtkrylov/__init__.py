@@ -409,6 +409,22 @@ class LineJacobi:
     def handle(self):
         return self._h
 
+    @property
+    def compact(self) -> bool:
+        """Apply forms l and g from the lines' constant x-couplings (reads only m)."""
+        u = C.c_int()
+        check(lib().vtk_linejacobi_get_compact(self._h, C.byref(u), None), self.A.ctx.handle)
+        return bool(u.value)
+
+    @property
+    def compact_available(self) -> bool:
+        a = C.c_int()
+        check(lib().vtk_linejacobi_get_compact(self._h, None, C.byref(a)), self.A.ctx.handle)
+        return bool(a.value)
+
+    def set_compact(self, on: bool):
+        check(lib().vtk_linejacobi_set_compact(self._h, int(bool(on))), self.A.ctx.handle)
+
     def factors(self) -> np.ndarray:
         """l | m | g, 3 * n_local doubles (the oracle's orc_line_setup layout)."""
         f = np.empty(3 * self.A.n_local)

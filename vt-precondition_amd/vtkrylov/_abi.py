@@ -89,6 +89,8 @@ PROTOTYPES = {
     "vtk_linejacobi_create": (C.c_int, [P, C.c_int64, C.c_int64, C.POINTER(P)]),
     "vtk_linejacobi_factors": (C.c_int, [P, P, C.c_int]),
     "vtk_prec_apply": (C.c_int, [P, P, P, C.c_int]),
+    "vtk_linejacobi_set_compact": (C.c_int, [P, C.c_int]),
+    "vtk_linejacobi_get_compact": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_kind_of": (C.c_int, [P, C.POINTER(C.c_int)]),
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
                             C.POINTER(C.c_int), C.POINTER(Stats)]),
