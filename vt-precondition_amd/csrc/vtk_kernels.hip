@@ -497,8 +497,14 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_DC_WLATE
 #define VTK_DC_WLATE 0
 #endif
+#ifndef VTK_SELL_SWZ
+#define VTK_SELL_SWZ 0   // XCD-aware group order (xcd_swizzle)
+#endif
+#ifndef VTK_SELL_WPE
+#define VTK_SELL_WPE 4   // minimum waves/SIMD the SELL kernels are register-limited to
+#endif
 template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_sell(SpmvK<VT, HALO> a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE))) void k_sell(SpmvK<VT, HALO> a) {
     constexpr int PSW = EPI == EPI_PREC_DC ? VTK_DC_PSW : 8;   // entries per load batch (DC: registers)
     constexpr int KB = VTK_DC_KB;   // basis vectors per load batch (DC)
     constexpr int JB = VTK_DC_JB;   // basis vectors with per-lane register accumulators (DC)
@@ -517,7 +523,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
         for (int k = 0; k < JB; ++k) { as_[k] = 0.0; az_[k] = 0.0; }
     }
-    for (int t = blockIdx.x; t < a.ngroups; t += gridDim.x) {
+    const int t0 = VTK_SELL_SWZ ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    for (int t = t0; t < a.ngroups; t += gridDim.x) {
         const int g = a.group_list ? a.group_list[t] : t;
         const int q = VTK_SCALAR_Q ? __builtin_amdgcn_readfirstlane(4 * g + wv) : 4 * g + wv;
         const int row = 64 * q + lane;
