@@ -1863,6 +1863,9 @@ hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, i
 // column j (c' = (e - H_j s)/r, e = [z; (beta - s.z)/r]) and nu_{j+1} = sqrt(gamma - e.e)/r;
 // ONE update pass writes v_j and p_{j+1} = (w - [V_j v_j] e) / (r nu).  Derivation: DESIGN.md.
 // ------------------------------------------------------------------------------------------
+#ifndef VTK_DOTS_WAVESPLIT
+#define VTK_DOTS_WAVESPLIT 0   // 1: the basis split over the waves (k_dc_dots) instead of rows
+#endif
 __global__ __launch_bounds__(NT) void k_dc_dots(const double *__restrict__ V, int64_t ld, int j,
                                                 const double *__restrict__ w, int64_t n, double *part,
                                                 const int *stop_col, int col) {
@@ -1930,10 +1933,90 @@ __global__ __launch_bounds__(NT) void k_dc_dots(const double *__restrict__ V, in
     }
 }
 
+// The same dots with every thread owning row pairs (as k_dc_update): p and w are read once per
+// row instead of once per wave, every basis vector streams through 16-B non-temporal loads and
+// the thread keeps JM >= j accumulators per quantity.  Same partial layout.
+template <int JM>
+__global__ __launch_bounds__(NT) void k_dc_dots_rows(const double *__restrict__ V, int64_t ld, int j,
+                                                     const double *__restrict__ w, int64_t n, double *part,
+                                                     const int *stop_col, int col) {
+    __shared__ double red[NT / 64][DC_NQ];
+    if (stopped(stop_col, col)) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double *p = V + (size_t)j * ld;
+    double as[JM], az[JM];
+#pragma unroll
+    for (int k = 0; k < JM; ++k) { as[k] = 0.0; az[k] = 0.0; }
+    double aa = 0.0, ab = 0.0, ag = 0.0;
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        const bool two = i + 1 < n;
+        double2 pv, wv2 = make_double2(0.0, 0.0);
+        if (two) {
+            pv = *reinterpret_cast<const double2 *>(p + i);
+            if (w) wv2 = *reinterpret_cast<const double2 *>(w + i);
+        } else {
+            pv = make_double2(p[i], 0.0);
+            if (w) wv2 = make_double2(w[i], 0.0);
+        }
+#pragma unroll
+        for (int k = 0; k < JM; ++k) {
+            if (k < j) {
+                const double *vk = V + (size_t)k * ld + i;
+                d2v v;
+                if (two) v = ldnt2(vk);
+                else { v.x = vk[0]; v.y = 0.0; }
+                as[k] += v.x * pv.x;
+                as[k] += v.y * pv.y;
+                if (w) {
+                    az[k] += v.x * wv2.x;
+                    az[k] += v.y * wv2.y;
+                }
+            }
+        }
+        aa += pv.x * pv.x;
+        aa += pv.y * pv.y;
+        if (w) {
+            ab += pv.x * wv2.x;
+            ab += pv.y * wv2.y;
+            ag += wv2.x * wv2.x;
+            ag += wv2.y * wv2.y;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < JM; ++k) {
+        if (k < j) {   // wave-uniform
+            const double ts = wave_sum(as[k]);
+            const double tz = w ? wave_sum(az[k]) : 0.0;
+            if (lane == 0) { red[wv][k] = ts; red[wv][DC_MAXJ + k] = tz; }
+        }
+    }
+    {
+        const double t0 = wave_sum(aa), t1 = wave_sum(ab), t2 = wave_sum(ag);
+        if (lane == 0) { red[wv][2 * DC_MAXJ] = t0; red[wv][2 * DC_MAXJ + 1] = t1; red[wv][2 * DC_MAXJ + 2] = t2; }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < DC_NQ; q += NT) {
+        const bool used = q < j || (q >= DC_MAXJ && q < DC_MAXJ + j && w) || q == 2 * DC_MAXJ ||
+                          (w && q > 2 * DC_MAXJ);
+        if (used) {
+            double t = 0.0;
+#pragma unroll
+            for (int w2 = 0; w2 < NT / 64; ++w2) t += red[w2][q];
+            part[(size_t)q * GMAX + blockIdx.x] = t;
+        }
+    }
+}
+
 hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, int64_t n, double *part,
                           int grid, const int *stop_col, int col, hipStream_t s) {
     if (j > DC_MAXJ) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_dc_dots, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, part, stop_col, col);
+    const dim3 g(grid), b(NT);
+    if (VTK_DOTS_WAVESPLIT) hipLaunchKernelGGL(k_dc_dots, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
+    else if (j <= 8) hipLaunchKernelGGL(k_dc_dots_rows<8>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
+    else if (j <= 16) hipLaunchKernelGGL(k_dc_dots_rows<16>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
+    else if (j <= 24) hipLaunchKernelGGL(k_dc_dots_rows<24>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
+    else hipLaunchKernelGGL(k_dc_dots_rows<DC_MAXJ>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
     return hipGetLastError();
 }
 
