@@ -588,6 +588,10 @@ void destroy_csr(vtk_csr *A) {
 
 // ---- GMRES -----------------------------------------------------------------------------------
 
+#ifndef VTK_DC_FUSED
+#define VTK_DC_FUSED 1   // DCGS2 dots inside the SpMV + BJ kernel (0: SpMV + BJ, then k_dc_dots)
+#endif
+
 struct Solver {
     vtk_csr *A;
     vtk_prec *M;
@@ -650,7 +654,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // every kernel of step j is tagged j: it returns at entry once stop_col < j
     // SpMV + BJ and the step's dots in one pass for BJ-fused tiles with bs <= 8 (larger blocks
     // would spill the fused kernel's registers)
-    const bool fused = bj_fused(s.M) && s.M->bs <= 8;
+    const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8;
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = matrix_bytes(s.A);
     const double b_inv = bj_row_bytes(s.M) * n;

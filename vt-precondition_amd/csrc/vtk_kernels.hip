@@ -22,10 +22,9 @@ namespace vtk {
 // ------------------------------------------------------------------------------------------
 // reductions
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_allsum(double v);
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    return v;  // lane 0
+    return wave_allsum(v);  // (every lane; callers read lane 0)
 }
 
 // every thread of the workgroup returns the same total (fixed order)
@@ -120,6 +119,48 @@ __device__ __forceinline__ double xload(const SpmvK<VT, HALO> &a, int c) {
     return a.x[c];
 }
 
+// ------------------------------------------------------------------------------------------
+// DPP lane moves (CDNA row-level data-parallel primitives: 16-lane rows, a VALU modifier
+// instead of an LDS-crossbar ds_bpermute).  Lanes whose source falls outside their row read 0.
+// Only the transport changes: a scan written with these moves does the same IEEE operations.
+// ------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+constexpr int DPP_ROW_SHL = 0x100;   // + n: lane i <- lane i + n of its row
+constexpr int DPP_ROW_SHR = 0x110;   // + n: lane i <- lane i - n of its row
+// __shfl_up / __shfl_down within groups of W <= 16 lanes (W divides 16): the lanes a group
+// would take from outside itself are exactly those the callers mask off
+template <int W>
+__device__ __forceinline__ double grp_up(double v, int off) {
+    if constexpr (W <= 16) {
+        switch (off) {
+            case 1: return dpp_mov<DPP_ROW_SHR + 1>(v);
+            case 2: return dpp_mov<DPP_ROW_SHR + 2>(v);
+            case 4: return dpp_mov<DPP_ROW_SHR + 4>(v);
+            default: return dpp_mov<DPP_ROW_SHR + 8>(v);
+        }
+    } else {
+        return __shfl_up(v, off, W);
+    }
+}
+template <int W>
+__device__ __forceinline__ double grp_down(double v, int off) {
+    if constexpr (W <= 16) {
+        switch (off) {
+            case 1: return dpp_mov<DPP_ROW_SHL + 1>(v);
+            case 2: return dpp_mov<DPP_ROW_SHL + 2>(v);
+            case 4: return dpp_mov<DPP_ROW_SHL + 4>(v);
+            default: return dpp_mov<DPP_ROW_SHL + 8>(v);
+        }
+    } else {
+        return __shfl_down(v, off, W);
+    }
+}
+
 template <int BS>
 __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]) {
     if constexpr (BS % 2 == 0) {
@@ -152,7 +193,7 @@ __device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, 
     double A = y, B = -l;
 #pragma unroll
     for (int off = 1; off < BS; off <<= 1) {
-        const double Ap = __shfl_up(A, off, BS), Bp = __shfl_up(B, off, BS);
+        const double Ap = grp_up<BS>(A, off), Bp = grp_up<BS>(B, off);
         if (ii >= off) {
             A = A + B * Ap;
             B = B * Bp;
@@ -162,7 +203,7 @@ __device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, 
     B = -g;
 #pragma unroll
     for (int off = 1; off < BS; off <<= 1) {
-        const double An = __shfl_down(A, off, BS), Bn = __shfl_down(B, off, BS);
+        const double An = grp_down<BS>(A, off), Bn = grp_down<BS>(B, off);
         if (ii + off < BS) {
             A = A + B * An;
             B = B * Bn;
@@ -177,13 +218,13 @@ __device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, 
 template <int BS>
 __device__ __forceinline__ double bj_trim_group(double y, int lane, double sub, double sup, double m) {
     const int ii = lane & (BS - 1);
-    const double mprev = __shfl_up(m, 1, BS);
+    const double mprev = grp_up<BS>(m, 1);
     const double l = ii > 0 ? sub * mprev : 0.0;
     const double g = sup * m;
     double A = y, B = -l;
 #pragma unroll
     for (int off = 1; off < BS; off <<= 1) {
-        const double Ap = __shfl_up(A, off, BS), Bp = __shfl_up(B, off, BS);
+        const double Ap = grp_up<BS>(A, off), Bp = grp_up<BS>(B, off);
         if (ii >= off) {
             A = A + B * Ap;
             B = B * Bp;
@@ -193,7 +234,7 @@ __device__ __forceinline__ double bj_trim_group(double y, int lane, double sub, 
     B = -g;
 #pragma unroll
     for (int off = 1; off < BS; off <<= 1) {
-        const double An = __shfl_down(A, off, BS), Bn = __shfl_down(B, off, BS);
+        const double An = grp_down<BS>(A, off), Bn = grp_down<BS>(B, off);
         if (ii + off < BS) {
             A = A + B * An;
             B = B * Bn;
@@ -470,10 +511,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // ~360 us + 29 us per register vector.  Tried and measured slower on one box (A/B): 20
 // register vectors at 3 waves/SIMD (-2 %), k >= 10 handed to k_dc_dots (-3 %).
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+// sum over the wavefront, the same bits in every lane: xor-1/xor-2 quad permutes, half-row and
+// row mirrors (each step adds a lane pair that both end up equal, a + b = b + a), then the four
+// row sums in a fixed order.  DPP moves and readlanes: no LDS traffic.
 __device__ __forceinline__ double wave_allsum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v = v + dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = v + dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = v + dpp_mov<0x141>(v);   // row_half_mirror
+    v = v + dpp_mov<0x140>(v);   // row_mirror
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 #ifndef VTK_DC_KB
