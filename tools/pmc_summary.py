@@ -31,7 +31,8 @@ CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output
     "spmv_resid_bj": "void vtk::k_sell<double, false, 3, 8, true>",
     "spmv_csr": "void vtk::k_spmv<double, false, 0, 1",
     "spmv_bj_dc_csr": "void vtk::k_spmv<double, false, 4, 8",
-    "dc_dots": "vtk::k_dc_dots(",
+    "dc_dots": "void vtk::k_dc_dots_rows<",
+    "line_apply": "void vtk::k_line_apply<",
     "dc_update": "vtk::k_dc_update(",
     "dc_scalar": "vtk::k_dc_scalar(",
     "mgs": "vtk::k_mgs(",
