@@ -548,6 +548,9 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_DC_WLATE
 #define VTK_DC_WLATE 0
 #endif
+#ifndef VTK_DC_VPRE
+#define VTK_DC_VPRE 1   // first basis batch loaded ahead of the SpMV (DC; A/B: -0.3 %..-0.6 % time)
+#endif
 #ifndef VTK_SELL_SWZ
 #define VTK_SELL_SWZ 0   // XCD-aware group order (xcd_swizzle)
 #endif
@@ -591,6 +594,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 if constexpr (TRIM) mrow = a.tri[a.tri_ld + row];
                 pv = a.x[row];
             }
+        }
+        // VPRE: the first batch of basis rows is loaded before the SpMV (no dependence on it),
+        // in flight during the gather chain
+        [[maybe_unused]] double vpre[(DC && VTK_DC_VPRE) ? KB : 1];
+        if constexpr (DC && VTK_DC_VPRE) {
+#pragma unroll
+            for (int u = 0; u < KB; ++u)
+                vpre[u] = (u < JB && u < a.j && act) ? __builtin_nontemporal_load(a.V + row + (size_t)u * a.ld) : 0.0;
         }
         if (64 * q < a.n_local) {
             const int64_t o0 = a.sell_off[q];
@@ -666,9 +677,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 if (k0 >= a.j) break;   // wave-uniform
                 double v[KB];
 #pragma unroll
-                for (int u = 0; u < KB; ++u)
+                for (int u = 0; u < KB; ++u) {
+                    if constexpr (VTK_DC_VPRE) {
+                        if (k0 == 0) {
+                            v[u] = vpre[u];
+                            continue;
+                        }
+                    }
                     v[u] = (k0 + u < JB && k0 + u < a.j && act)
                                ? __builtin_nontemporal_load(vb + (size_t)(k0 + u) * a.ld) : 0.0;
+                }
 #pragma unroll
                 for (int u = 0; u < KB; ++u) {
                     if (k0 + u < JB) {   // compile-time after unrolling: JB need not divide by KB
