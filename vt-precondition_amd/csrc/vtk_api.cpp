@@ -784,11 +784,21 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     Red rb = reduce(c, s.part[0], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rb, &ds->scal[0], 1, c->stream));
+    // M b goes to V[0]: with x0 = 0 it is the first cycle's psolve(r) (below)
     { Prof pf(c, prec_cls(M), -1, b_pc);
-      HIPCHK(c, launch_bj_apply(bj_op(M), n, b, s.w, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream)); }
+      HIPCHK(c, launch_bj_apply(bj_op(M), n, b, s.V, nullptr, s.part[1], nullptr, s.G, nullptr, 0, c->stream)); }
     Red rmb = reduce(c, s.part[1], s.G, rc);
     TRY(rc);
     HIPCHK(c, launch_finalize(rmb, &ds->scal[1], 1, c->stream));
+    // `r = b - matvec(x) if x.any() else b.copy()` (iterative.py:737): any nonzero x0 on any rank
+    HIPCHK(c, hipMemsetAsync(&ds->scal[2], 0, sizeof(double), c->stream));
+    { Prof pf(c, "any", -1, n8);
+      HIPCHK(c, launch_any_nonzero(x, n, &ds->scal[2], c->stream)); }
+    if (c->dist) TRY(comm_allreduce(c, &ds->scal[2], 1));
+    double x_any = 0.0;
+    HIPCHK(c, hipMemcpyAsync(&x_any, &ds->scal[2], sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const bool r_is_b = x_any == 0.0;
     // r = b - A x (iterative.py:737, :816).  When the BJ tiles allow (or M is the identity) the
     // residual kernel also applies M^-1 and writes v0's direction straight into V[0]: the next
     // cycle's psolve(r) (:742) is then already done.
@@ -819,7 +829,13 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         HIPCHK(c, launch_finalize(rr, &ds->rnorm, 1, c->stream));
         return VTK_OK;
     };
-    TRY(residual());
+    if (r_is_b) {
+        // r = b: ||r|| = ||b||, and psolve(r) = M b is already in V[0] with its partials
+        HIPCHK(c, hipMemcpyAsync(&ds->rnorm, &ds->scal[0], sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        rz = Red{s.part[1], s.G};
+    } else {
+        TRY(residual());
+    }
     HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const double bnrm2 = hs->scal[0], Mb_nrm2 = hs->scal[1];
@@ -858,7 +874,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         hs->ptol = ptol;
         HIPCHK(c, hipMemcpyAsync(&ds->ptol, &hs->ptol, sizeof(double), hipMemcpyHostToDevice, c->stream));
         Red rv = rz;
-        if (!fres) {
+        if (!fres && !(it == 0 && r_is_b)) {
             { Prof pf(c, prec_cls(M), -1, b_pc);
               HIPCHK(c, launch_bj_apply(bj_op(M), n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
             rv = reduce(c, s.part[0], s.G, rc);

@@ -279,6 +279,8 @@ hipError_t launch_finalize(Red p, double *dst, int do_sqrt, hipStream_t s);
 // part = sum x^2 (or x*y)
 hipError_t launch_dot(const double *x, const double *y, int64_t n, double *part, int grid,
                       hipStream_t s);
+// *flag = 1.0 when some x[i] != 0 (zeroed by the caller)
+hipError_t launch_any_nonzero(const double *x, int64_t n, double *flag, hipStream_t s);
 hipError_t launch_gather(const double *x, const int32_t *idx, int64_t cnt, double *out,
                          hipStream_t s);
 // device operator assembly

@@ -1833,6 +1833,19 @@ __global__ __launch_bounds__(NT) void k_dot(const double *__restrict__ x, const 
     if (threadIdx.x == 0) part[blockIdx.x] = t;
 }
 
+// *flag = 1.0 if any x[i] != 0 (NaN counts as nonzero, as numpy's any); the caller zeroes it
+__global__ __launch_bounds__(NT) void k_any_nonzero(const double *__restrict__ x, int64_t n, double *flag) {
+    bool nz = false;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) nz |= x[i] != 0.0;
+    if (__any(nz) && (threadIdx.x & 63) == 0) *flag = 1.0;   // every writer stores the same value
+}
+
+hipError_t launch_any_nonzero(const double *x, int64_t n, double *flag, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_any_nonzero, dim3(vector_grid(n)), dim3(NT), 0, s, x, n, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_dot(const double *x, const double *y, int64_t n, double *part, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_dot, dim3(grid), dim3(NT), 0, s, x, y, n, part);
     return hipGetLastError();
