@@ -324,13 +324,14 @@ __device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, dou
 template <typename VT, bool HALO, int EPI, int BS, bool TRI, bool TRIM = false>
 __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double s, int row, bool act, int lane,
                                                double &acc0, double &acc1, double sub = 0.0, double sup = 0.0,
-                                               bool have_m = false, double mrow = 1.0, bool store = true) {
+                                               bool have_m = false, double mrow = 1.0, bool store = true,
+                                               bool have_bv = false, double bv = 0.0, double v0v = 0.0) {
     constexpr bool DC = EPI == EPI_PREC_DC;
     if constexpr (EPI == EPI_PLAIN) {
         if (act) a.y[row] = s;
         return s;
     } else if constexpr (EPI == EPI_RESID) {
-        const double r = act ? a.b[row] - s : 0.0;
+        const double r = act ? (have_bv ? bv : a.b[row]) - s : 0.0;
         if (act) {
             a.y[row] = r;
             acc0 += r * r;
@@ -340,7 +341,7 @@ __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double 
         // PREC: z = M^-1 (A x);  RESID_PREC: r = b - A x (iterative.py:816), z = M^-1 r
         double sv = s;
         if constexpr (EPI == EPI_RESID_PREC) {
-            sv = act ? a.b[row] - s : 0.0;
+            sv = act ? (have_bv ? bv : a.b[row]) - s : 0.0;
             acc0 += sv * sv;
         }
         double z = sv;
@@ -367,7 +368,7 @@ __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double 
                 acc1 += z * z;
             } else if constexpr (!DC) {
                 acc0 += z * z;
-                if (a.v0) acc1 += a.v0[row] * z;
+                if (a.v0) acc1 += (have_bv ? v0v : a.v0[row]) * z;
             }
         }
         return act ? z : 0.0;
@@ -548,6 +549,9 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_DC_WLATE
 #define VTK_DC_WLATE 0
 #endif
+#ifndef VTK_EPI_HOIST
+#define VTK_EPI_HOIST 1   // RESID / PREC / RESID_PREC: the row's m, b, v0 loaded ahead of the SpMV
+#endif
 #ifndef VTK_DC_VPRE
 #define VTK_DC_VPRE 1   // first basis batch loaded ahead of the SpMV (DC; A/B: -0.3 %..-0.6 % time)
 #endif
@@ -564,6 +568,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
     constexpr int JB = VTK_DC_JB;   // basis vectors with per-lane register accumulators (DC)
     constexpr bool DC = EPI == EPI_PREC_DC;
     constexpr bool HOIST = DC && VTK_DC_HOIST;
+    constexpr bool HOISTE = !DC && EPI != EPI_PLAIN && VTK_EPI_HOIST;   // the other epilogues
     constexpr bool WLATE = DC && VTK_DC_WLATE;
     constexpr int NQW = 2 * DC_MAXJ + 3;      // per-wave partial record (DC)
     __shared__ double stage[(NT / 64) * NQW];
@@ -587,12 +592,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         double sub = 0.0, sup = 0.0;   // TRI: the row's block sub/super-diagonal entries
         constexpr bool TRIM = TRI && BS > 0;
         [[maybe_unused]] const int ii = lane & (BS > 0 ? BS - 1 : 0);
-        // HOIST: the row's own operands (BJ factor, p) issued ahead of the CSR loads
-        double mrow = 1.0, pv = 0.0;
+        // HOIST: the row's own operands (BJ factor m, p, b, v0) issued ahead of the CSR loads,
+        // so the epilogue does not wait a memory round trip per chunk (EPI_PREC: 352 -> ... us)
+        double mrow = 1.0, pv = 0.0, bv = 0.0, v0v = 0.0;
         if constexpr (HOIST) {
             if (act) {
                 if constexpr (TRIM) mrow = a.tri[a.tri_ld + row];
                 pv = a.x[row];
+            }
+        } else if constexpr (HOISTE) {
+            if (act) {
+                if constexpr (TRIM) mrow = a.tri[a.tri_ld + row];
+                if constexpr (EPI == EPI_RESID || EPI == EPI_RESID_PREC) bv = a.b[row];
+                if constexpr (EPI == EPI_PREC) {
+                    if (a.v0) v0v = a.v0[row];
+                }
             }
         }
         // VPRE: the first batch of basis rows is loaded before the SpMV (no dependence on it),
@@ -665,7 +679,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
             }
         }
         const double z = row_epilogue<VT, HALO, EPI, BS, TRI, TRIM>(a, s, row, act, lane, acc0, acc1, sub, sup,
-                                                                    HOIST && TRIM, mrow, !WLATE);
+                                                                    (HOIST || HOISTE) && TRIM, mrow, !WLATE,
+                                                                    HOISTE, bv, v0v);
         if constexpr (DC) {
             if constexpr (!HOIST) pv = act ? a.x[row] : 0.0;   // p_j (= the SpMV input) on this row
             daa += pv * pv;
