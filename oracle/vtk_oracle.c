@@ -271,8 +271,7 @@ static int line_has(int64_t R, int64_t d, int64_t row0, int64_t n, int64_t strid
 
 int64_t orc_line_setup(int64_t n, const int32_t *indptr, const int32_t *indices, const void *data,
                        int fp32, int64_t row0, int64_t stride, int64_t seg, double *f) {
-    double *u = (double *)malloc(sizeof(double) * (n ? n : 1));
-    double *cs = (double *)malloc(sizeof(double) * (n ? n : 1));
+    double *cs = (double *)malloc(sizeof(double) * (n ? n : 1));   /* c of each row */
     double *l = f, *mm = f + n, *g = f + 2 * n;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t R = row0 + r;
@@ -293,14 +292,12 @@ int64_t orc_line_setup(int64_t n, const int32_t *indptr, const int32_t *indices,
             uv = b;
         }
         const double mv = 1.0 / uv;
-        if (uv == 0.0 || !isfinite(uv) || !isfinite(mv)) { free(u); free(cs); return -(r + 1); }
-        u[r] = uv;
+        if (uv == 0.0 || !isfinite(uv) || !isfinite(mv)) { free(cs); return -(r + 1); }
         cs[r] = c;
         l[r] = lv;
         mm[r] = mv;
         g[r] = c * mv;
     }
-    free(u);
     free(cs);
     return 0;
 }
