@@ -561,9 +561,10 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_SELL_WPE
 #define VTK_SELL_WPE 4   // minimum waves/SIMD the SELL kernels are register-limited to
 #endif
-template <typename VT, bool HALO, int EPI, int BS, bool TRI = false>
+template <typename VT, bool HALO, int EPI, int BS, bool TRI = false, int PSWT = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE))) void k_sell(SpmvK<VT, HALO> a) {
-    constexpr int PSW = EPI == EPI_PREC_DC ? VTK_DC_PSW : 8;   // entries per load batch (DC: registers)
+    // entries per load batch (DC: registers; PSWT: a row length the launch picked)
+    constexpr int PSW = EPI == EPI_PREC_DC ? (PSWT > 0 ? PSWT : VTK_DC_PSW) : 8;
     constexpr int KB = VTK_DC_KB;   // basis vectors per load batch (DC)
     constexpr int JB = VTK_DC_JB;   // basis vectors with per-lane register accumulators (DC)
     constexpr bool DC = EPI == EPI_PREC_DC;
@@ -992,8 +993,15 @@ static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, 
     // BJ-fused tiles only (bs 1..8); the host falls back to the unfused dots otherwise
     const int bs = (bj.inv || bj.tri) ? bj.bs : 0;
     if (bs == 0) return hipErrorInvalidValue;
-    return launch_bj_variant<VT, HALO, EPI_PREC_DC, 8>(a, bs, bj.tri != nullptr, in.sell && in.groups,
-                                                       dim3(spmv_grid(in)), s);
+    // SELL chunks of <= 5 entries per row on average (the 2D operators: 5-point rows): one load
+    // batch of 5 covers a row (C3 fused step 621 -> 590 us); wider rows keep batches of 4 (C4:
+    // 5 would cost +5 %)
+    const bool sell = in.sell && in.groups;
+    if (sell && bj.tri && bs == 8 && in.sell->nch > 0 && in.sell->entries <= in.sell->nch * 64 * 5) {
+        hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, 5>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        return hipGetLastError();
+    }
+    return launch_bj_variant<VT, HALO, EPI_PREC_DC, 8>(a, bs, bj.tri != nullptr, sell, dim3(spmv_grid(in)), s);
 }
 
 hipError_t launch_spmv_dc(const SpmvIn &in, double *w, const BjOp &bj, const double *V,
