@@ -82,6 +82,26 @@ __device__ __forceinline__ d2v ldnt2(const double *p) {
 #ifndef VTK_NT_MISC
 #define VTK_NT_MISC 6
 #endif
+// non-temporal loads of operands read once per kernel (VTK_NT_LOADS bits: 1 fused BJ m,
+// 2 update p/w, 4 dots p/w, 8 line apply r/m).  A/B: 1 = +2.5 % (C3 BJ path), 4|8 = +1 %
+// (line path), 2 = +2 % line but -1 % BJ (off)
+#ifndef VTK_NT_LOADS
+#define VTK_NT_LOADS 13
+#endif
+template <int BIT>
+__device__ __forceinline__ double ld_nt(const double *p) {
+    if constexpr ((VTK_NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int BIT>
+__device__ __forceinline__ double2 ld_nt2(const double *p) {
+    if constexpr ((VTK_NT_LOADS & BIT) != 0) {
+        const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+        return make_double2(v.x, v.y);
+    } else {
+        return *reinterpret_cast<const double2 *>(p);
+    }
+}
 template <int BIT>
 __device__ __forceinline__ void st_nt(double *p, double v) {
     if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(v, p);
@@ -620,12 +640,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         double mrow = 1.0, pv = 0.0, bv = 0.0, v0v = 0.0;
         if constexpr (HOIST) {
             if (act) {
-                if constexpr (TRIM) mrow = a.tri[a.tri_ld + row];
+                if constexpr (TRIM) mrow = ld_nt<1>(a.tri + a.tri_ld + row);
                 pv = a.x[row];
             }
         } else if constexpr (HOISTE) {
             if (act) {
-                if constexpr (TRIM) mrow = a.tri[a.tri_ld + row];
+                if constexpr (TRIM) mrow = ld_nt<1>(a.tri + a.tri_ld + row);
                 if constexpr (EPI == EPI_RESID || EPI == EPI_RESID_PREC) bv = a.b[row];
                 if constexpr (EPI == EPI_PREC) {
                     if (a.v0) v0v = a.v0[row];
@@ -1375,7 +1395,7 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
                 const int64_t kl = k0l + (int64_t)u * S;
                 const bool ok = q.jv && u < len && kl >= 0 && kl < nn;
                 const int k = ok ? (int)kl : 0;
-                const double mv = m[k];
+                const double mv = ld_nt<8>(m + k);
                 double lv, gv;
                 if constexpr (COMPACT) {
                     const bool hl = ok && pok;
@@ -1386,7 +1406,7 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
                     lv = l[k];
                     gv = g[k];
                 }
-                const double dv = r[k] - lv * dp;
+                const double dv = ld_nt<8>(r + k) - lv * dp;
                 e[u] = mv * dv;
                 gg[u] = gv;
                 if (ok) {
@@ -2080,8 +2100,8 @@ __global__ __launch_bounds__(NT) void k_dc_dots_rows(const double *__restrict__ 
         const bool two = i + 1 < n;
         double2 pv, wv2 = make_double2(0.0, 0.0);
         if (two) {
-            pv = *reinterpret_cast<const double2 *>(p + i);
-            if (w) wv2 = *reinterpret_cast<const double2 *>(w + i);
+            pv = ld_nt2<4>(p + i);
+            if (w) wv2 = ld_nt2<4>(w + i);
         } else {
             pv = make_double2(p[i], 0.0);
             if (w) wv2 = make_double2(w[i], 0.0);
@@ -2402,8 +2422,8 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
     const int64_t stride = 2 * (int64_t)gridDim.x * NT;
     for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
         if (i + 1 < n) {
-            const double2 p = *reinterpret_cast<const double2 *>(pj + i);
-            double2 a = p, t = *reinterpret_cast<const double2 *>(w + i);
+            const double2 p = ld_nt2<2>(pj + i);
+            double2 a = p, t = ld_nt2<2>(w + i);
             for (int k = 0; k < j; ++k) {
                 const d2v v = ldnt2(V + (size_t)k * ld + i);
                 const double sk = cs[k], ek = ce[k];
