@@ -26,9 +26,9 @@ import statistics
 
 CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output (default path:
               # SELL-64 layout, tridiagonal-factor BJ(8), DCGS2)
-    "spmv_bj_dc": "void vtk::k_sell<double, false, 4, 8, true>",
-    "spmv": "void vtk::k_sell<double, false, 0, 1, false>",
-    "spmv_resid_bj": "void vtk::k_sell<double, false, 3, 8, true>",
+    "spmv_bj_dc": "void vtk::k_sell<double, false, 4, 8, true,",
+    "spmv": "void vtk::k_sell<double, false, 0, 1, false,",
+    "spmv_resid_bj": "void vtk::k_sell<double, false, 3, 8, true,",
     "spmv_csr": "void vtk::k_spmv<double, false, 0, 1",
     "spmv_bj_dc_csr": "void vtk::k_spmv<double, false, 4, 8",
     "dc_dots": "void vtk::k_dc_dots_rows<",
