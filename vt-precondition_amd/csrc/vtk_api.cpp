@@ -716,7 +716,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         }
         TRY(reduce_step(j, s.w, j, cnt));
         { Prof pf(c, "dc_update", j, n8 * (j + 4));
-          HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, c->stream)); }
+          HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, fused ? 0 : 1, c->stream)); }
         HIPCHK(c, hipEventRecord(ev[j % (LOOKAHEAD + 1)], c->stream));
         if (j >= LOOKAHEAD) {
             HIPCHK(c, hipEventSynchronize(ev[(j - LOOKAHEAD) % (LOOKAHEAD + 1)]));

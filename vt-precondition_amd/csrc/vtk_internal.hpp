@@ -310,7 +310,7 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
                             int closing, double *Hraw, double *H, double *S, double *giv,
                             DcCoef *cf, GmresState *st, int *stop_map, hipStream_t s);
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
-                            const DcCoef *cf, int grid, const int *stop_col, hipStream_t s);
+                            const DcCoef *cf, int grid, const int *stop_col, int nt_pw, hipStream_t s);
 
 int vector_grid(int64_t n);
 

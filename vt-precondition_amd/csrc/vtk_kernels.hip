@@ -83,8 +83,8 @@ __device__ __forceinline__ d2v ldnt2(const double *p) {
 #define VTK_NT_MISC 6
 #endif
 // non-temporal loads of operands read once per kernel (VTK_NT_LOADS bits: 1 fused BJ m,
-// 2 update p/w, 4 dots p/w, 8 line apply r/m).  A/B: 1 = +2.5 % (C3 BJ path), 4|8 = +1 %
-// (line path), 2 = +2 % line but -1 % BJ (off)
+// 4 dots p/w, 8 line apply r/m; the update pass chooses per path, k_dc_update<NTPW>).
+// A/B: 1 = +2.5 % (C3 BJ path), 4|8 = +1 % (line path)
 #ifndef VTK_NT_LOADS
 #define VTK_NT_LOADS 13
 #endif
@@ -2404,6 +2404,9 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 #ifndef VTK_UPD_NT
 #define VTK_UPD_NT 2   // non-temporal stores in the update pass: 1 v_j, 2 v_j and p_{j+1} (A/B: 2 = +2.6 % it/s)
 #endif
+// NTPW: p_j and w loaded non-temporal (A/B: +2 % on the unfused (line) path, -1 % after the
+// fused BJ step, whose w the update re-reads warm)
+template <bool NTPW>
 __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_t ld, int j,
                                                   const double *__restrict__ w, int64_t n,
                                                   const DcCoef *cf, const int *stop_col) {
@@ -2422,8 +2425,16 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
     const int64_t stride = 2 * (int64_t)gridDim.x * NT;
     for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
         if (i + 1 < n) {
-            const double2 p = ld_nt2<2>(pj + i);
-            double2 a = p, t = ld_nt2<2>(w + i);
+            double2 p, t;
+            if constexpr (NTPW) {
+                const d2v pp = ldnt2(pj + i), tt = ldnt2(w + i);
+                p = make_double2(pp.x, pp.y);
+                t = make_double2(tt.x, tt.y);
+            } else {
+                p = *reinterpret_cast<const double2 *>(pj + i);
+                t = *reinterpret_cast<const double2 *>(w + i);
+            }
+            double2 a = p;
             for (int k = 0; k < j; ++k) {
                 const d2v v = ldnt2(V + (size_t)k * ld + i);
                 const double sk = cs[k], ek = ce[k];
@@ -2462,8 +2473,12 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
 }
 
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n, const DcCoef *cf,
-                            int grid, const int *stop_col, hipStream_t s) {
-    hipLaunchKernelGGL(k_dc_update, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, stop_col);
+                            int grid, const int *stop_col, int nt_pw, hipStream_t s) {
+#ifdef VTK_UPD_NTPW_FORCE
+    nt_pw = VTK_UPD_NTPW_FORCE;
+#endif
+    if (nt_pw) hipLaunchKernelGGL(k_dc_update<true>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, stop_col);
+    else hipLaunchKernelGGL(k_dc_update<false>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, stop_col);
     return hipGetLastError();
 }
 
