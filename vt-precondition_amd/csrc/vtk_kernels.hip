@@ -594,6 +594,9 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_EPI_HOIST
 #define VTK_EPI_HOIST 1   // RESID / PREC / RESID_PREC: the row's m, b, v0 loaded ahead of the SpMV
 #endif
+#ifndef VTK_WORD_EARLY
+#define VTK_WORD_EARLY 1   // first code word loaded with the dictionary (A/B: fused -1 %, residual -6 %)
+#endif
 #ifndef VTK_DC_VPRE
 #define VTK_DC_VPRE 1   // first basis batch loaded ahead of the SpMV (DC; A/B: -0.3 %..-0.6 % time)
 #endif
@@ -685,14 +688,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
             // for "wide" chunks / unpacked copies; wave-uniform choice, one code path
             bool wide = true;
             int dv = 0;
+            // WORD_EARLY: the first code word is loaded together with the dictionary (every chunk
+            // has its pk words, wide or not), not after the wide test has seen the dictionary
+            const uint32_t *pw = a.pk ? a.pk + a.pk_off[q] + lane : nullptr;
+            const uint32_t word0 = (VTK_WORD_EARLY && a.pk && w > 0) ? __builtin_nontemporal_load(pw) : 0u;
             if (a.pk) {   // the chunk's dictionary: one 64-B load by lanes 0..15
                 dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
                 wide = __shfl(dv, 15, 64) != 0;
             }
             const int32_t *cc = a.sell_col + o0 + lane;
-            const uint32_t *pw = wide ? nullptr : a.pk + a.pk_off[q] + lane;
             for (int k0 = 0; k0 < w; k0 += 8) {
-                const uint32_t word = wide ? 0u : __builtin_nontemporal_load(pw + (k0 >> 3) * 64);
+                const uint32_t word = wide ? 0u
+                                           : ((VTK_WORD_EARLY && k0 == 0) ? word0
+                                                                          : __builtin_nontemporal_load(pw + (k0 >> 3) * 64));
 #pragma unroll
                 for (int h = 0; h < 8; h += PSW) {
                     if (k0 + h >= w) break;   // wave-uniform
