@@ -455,6 +455,16 @@ int build_sell(vtk_csr *A, bool only_if_compact, bool *built) {
     if (e != hipSuccess) { drop(); return fail(c, e == hipErrorOutOfMemory ? VTK_ERR_NOMEM : VTK_ERR_HIP,
                                               std::string("SELL build: ") + hipGetErrorString(e)); }
     sl.nch = nch;
+    // uniform chunk width (the Vlasov operators: every 64-row chunk holds a full-stencil row)
+    {
+        std::vector<int64_t> off((size_t)nch + 1);
+        if (hipMemcpy(off.data(), sl.d_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost) == hipSuccess && nch > 0) {
+            const int64_t w0 = (off[1] - off[0]) >> 6;
+            bool uni = w0 > 0 && w0 < (1 << 20);
+            for (int64_t q = 1; q < nch && uni; ++q) uni = ((off[(size_t)q + 1] - off[(size_t)q]) >> 6) == w0;
+            sl.uniform_w = uni ? (int)w0 : 0;
+        }
+    }
     A->sell = sl;
     *built = true;
     return VTK_OK;

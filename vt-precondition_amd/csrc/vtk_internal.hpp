@@ -80,6 +80,7 @@ struct Sell {
     int64_t n_wide = 0;          // chunks that kept int32 columns
     int64_t wide_entries = 0;    // their entries (64 per row slot)
     int64_t pk_words = 0;
+    int uniform_w = 0;           // every chunk has this width (offsets are 64 W q): no offset loads
 };
 constexpr int PK_CODES = 15;     // offsets per chunk dictionary (codes 0..14; 15 = padding)
 
