@@ -33,7 +33,7 @@ CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output
     "spmv_bj_dc_csr": "void vtk::k_spmv<double, false, 4, 8",
     "dc_dots": "void vtk::k_dc_dots_rows<",
     "line_apply": "void vtk::k_line_apply<",
-    "dc_update": "vtk::k_dc_update(",
+    "dc_update": "void vtk::k_dc_update<",
     "dc_scalar": "vtk::k_dc_scalar(",
     "mgs": "vtk::k_mgs(",
     "tail": "vtk::k_tail(",
