@@ -37,6 +37,7 @@ for s in "$@"; do
         benchc1solo) step benchc1solo 300 python bench.py --config C1 --steps 5 --warmup 1 --no-cpu-baseline --comm-solo ;;
         gridscan) for G in 512 768 896 960 1000 1024; do VTK_SELL_GRID=$G step grid$G 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; done ;;
         profline) step profline 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profline -o run --output-format csv -- python bench.py --prec line --steps 3 --warmup 1 --no-cpu-baseline ;;
+        profc4) step profc4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc4 -o run --output-format csv -- python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 ;;
         profmgs) step profmgs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profmgs -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --orth mgs ;;
         ab) for v in a cur a cur; do if [ $v = a ]; then L=tools/bin/lib_a/libvtkrylov.so; else L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; fi; VTK_LIB=$L step ab_$v 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; grep -o '"value": [0-9.]*' gpurun_out/ab_$v.log; done ;;
         variants) for rep in 1 2; do for v in cur ${VARIANTS:-a}; do if [ $v = cur ]; then L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; else L=tools/bin/lib_$v/libvtkrylov.so; fi; VTK_LIB=$L step var_${v}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 ${BENCH_ARGS:-} || exit $?; python tools/bench_brief.py gpurun_out/var_${v}_$rep.log; done; done ;;
