@@ -193,8 +193,11 @@ def main():
     t = time.perf_counter()
     iters = 0
     infos = []
+    per_solve = []   # vtk_gmres returns synchronised: wall time per solve (SURVEY §8d median)
     for _ in range(args.steps):
+        ts = time.perf_counter()
         x, info, st = solve()
+        per_solve.append(time.perf_counter() - ts)
         iters += st.inner_iters
         infos.append(info)
     torch.cuda.synchronize()
@@ -238,7 +241,7 @@ def main():
     flush = torch.empty(512 * 2**20 // 8, dtype=torch.float64, device=dev)
     cold = []
     with torch.cuda.stream(stream):
-        for _ in range(min(args.spmv_reps, 20)):
+        for _ in range(max(20, min(2 * args.spmv_reps, 100))):   # 100 flushed reps
             flush.fill_(1.0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -330,6 +333,7 @@ def main():
                    "comm": args.comm if world > 1 else ("rccl-solo" if args.comm_solo else None)},
         "inner_iters_per_solve": iters / args.steps,
         "solves_per_s": args.steps / elapsed,
+        "solve_ms_median": sorted(per_solve)[len(per_solve) // 2] * 1e3,
         "info": infos,
         "true_rel_residual": rel_res,
         "spmv": {"gbs": spmv_gbs, "hbm_frac": spmv_gbs / HBM_PEAK_GBS, "us": t_spmv * 1e6, "bytes": B,
