@@ -5,6 +5,11 @@ rank per MI355X.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+With --gpus N > 1 and no launcher (WORLD_SIZE unset) the script starts its own N ranks: the
+parent process never touches the GPU, it spawns N fresh children (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one GPU each), passes rank 0's JSON line
+through and exits non-zero if any rank fails.
+
 A step = one full solve: x0 = 0 -> ||b - A x|| <= 1e-8 ||b|| with GMRES(20) + block-Jacobi(8)
 (SURVEY.md §8d).  value = inner (Arnoldi) iterations of the K timed solves / the max-over-ranks
 wall time of those solves.  The problem is fixed as N grows (strong scaling; rows sharded in
@@ -98,6 +103,44 @@ def cpu_baseline(cfg_name, A_host, b, bs, rtol, inner_limit, line=None):
     }
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start ranks 0..n-1 of this same command as child processes (the torch.distributed.run
+    environment contract) and wait for them.  Called before anything initialises the GPU; a
+    failing rank ends the others (exact PIDs), so a half-dead job cannot hang the barrier."""
+    import signal
+    import subprocess
+    env0 = dict(os.environ)
+    env0.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(free_port()), "GROUP_RANK": "0", "VTK_BENCH_SPAWNED": "1"})
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"[launcher] rank {procs.index(p)} exited with {code}: stopping the other ranks")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,7 +170,13 @@ def main():
                     help="one GPU through the distributed code paths (one-rank RCCL communicator)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="rank plumbing only (no GPU): init the process group, all-reduce the ranks, "
+                         "rank 0 prints one JSON line")
+    ap.add_argument("--check-launch-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))   # no GPU call has happened in this process
 
     import numpy as np
     import torch
@@ -141,6 +190,19 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    if args.check_launch:
+        if rank == args.check_launch_fail_rank:
+            raise SystemExit(3)
+        t = torch.tensor([rank, 1], dtype=torch.int64)
+        if dist is not None:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"check_launch": True, "n_gpus": world, "rank_sum": int(t[0]), "ranks": int(t[1]),
+                              "local_rank": local, "launcher": os.environ.get("VTK_BENCH_SPAWNED") and "bench.py"}),
+                  flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     import vtkrylov as vk
     from vtkrylov import comm as vkcomm
@@ -330,7 +392,9 @@ def main():
                    "prec": args.prec, "bs": args.bs if args.prec == "bj" else None,
                    "seg": args.seg if args.prec == "line" else None, "bj_apply": mmode, "layout": A.layout, "rtol": args.rtol, "orth": args.orth,
                    "parallelism": f"row-slab x{world}",
-                   "comm": args.comm if world > 1 else ("rccl-solo" if args.comm_solo else None)},
+                   "comm": args.comm if world > 1 else ("rccl-solo" if args.comm_solo else None),
+                   "launcher": ("bench.py" if os.environ.get("VTK_BENCH_SPAWNED") else "external") if world > 1 else None},
+        "rccl_ranks": ctx.rccl_ranks(),
         "inner_iters_per_solve": iters / args.steps,
         "solves_per_s": args.steps / elapsed,
         "solve_ms_median": sorted(per_solve)[len(per_solve) // 2] * 1e3,

@@ -162,6 +162,9 @@ typedef struct {
 } vtk_host_comm;
 int vtk_comm_init_host(vtk_ctx *ctx, int rank, int world, const vtk_host_comm *ops);
 int vtk_comm_info(vtk_ctx *ctx, int *rank, int *world);
+/* ranks of the context's RCCL communicator (ncclCommCount); 0 when the context has none
+ * (world 1, or the host-staged transport) */
+int vtk_comm_rccl_count(vtk_ctx *ctx, int *count);
 
 /* ---- operator ------------------------------------------------------------------------ */
 /* Row block [offsets[rank], offsets[rank+1]) of an n_global x n_global CSR matrix with

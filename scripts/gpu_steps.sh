@@ -49,6 +49,9 @@ for s in "$@"; do
         bench2host) step bench2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --comm host --config C1 --steps 1 --warmup 1 --spmv-reps 3 ;;
         profc1) step profc1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc1 -o run --output-format csv -- python bench.py --config C1 --steps 3 --warmup 1 --no-cpu-baseline ;;
         pmcsq) step pmcsq 120 rocprofv3 --pmc ${PMC:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES} -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 2 ;;
+        bench2self) step bench2self 600 python bench.py --gpus 2 --comm host --config C1 --steps 1 --warmup 1 --spmv-reps 3 --no-cpu-baseline ;;
+        pmcwc4) step pmcwc4 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_c4 -o run --output-format csv -- python bench.py --config C4 --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 3 ;;
+        pmcsqc4) step pmcsqc4 300 rocprofv3 --pmc ${PMC:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES} -d gpurun_out/pmc_sq_c4 -o run --output-format csv -- python bench.py --config C4 --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 3 ;;
         pmcfc4) step pmcfc4 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_c4 -o run --output-format csv -- python bench.py --config C4 --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 3 ;;
         pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
         pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;

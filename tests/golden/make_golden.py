@@ -210,12 +210,62 @@ def large(out, with_c4):
     print("wrote", out)
 
 
+def solve_summary(s_x, info, inner, true_resid, b_norm, **extra):
+    """What a full-size GPU parity test compares (tests/test_gpu_large.py): info, inner
+    iterations, ||x||, the first/last 8 entries and 64 entries sampled at a fixed stride."""
+    n = s_x.shape[0]
+    stride = max(1, n // 64)
+    return {"rtol": 1e-8, "restart": 20, "info": int(info), "inner_iters": int(inner),
+            "x_norm2": float(np.linalg.norm(s_x)), "true_resid": float(true_resid), "b_norm2": float(b_norm),
+            "x_first8": s_x[:8].tolist(), "x_last8": s_x[-8:].tolist(),
+            "x_sample_stride": stride, "x_sample": s_x[::stride][:64].tolist(), **extra}
+
+
+def gmres_large(out, names):
+    """SciPy GMRES(20) + BJ(8) to rtol 1e-8 at the headline sizes (C2, C3: the bench workload);
+    C4 (50M rows, fp32 values: SciPy would upcast a 3.6 GB copy of the values per SpMV) from
+    the C restatement, which is pinned to SciPy at C0/S2/S4/S4F/C1 (tests/test_oracle.py)."""
+    from oracle import coracle
+    with open(out) as f:
+        res = json.load(f)
+    for name in names:
+        p = twin.CONFIGS[name]
+        t = time.time()
+        if name == "C4":
+            ip, ix, d = coracle.generate(p)
+            b = coracle.rhs(p.n)
+            inv = coracle.bj_setup(ip, ix, d, 8)
+            r = coracle.gmres(ip, ix, d, b, inv, rtol=1e-8)
+            true_res = float(np.linalg.norm(b - coracle.spmv(ip, ix, d, r.x)))
+            summ = solve_summary(r.x, r.info, r.inner_iters, true_res, np.linalg.norm(b),
+                                 source="oracle/vtk_oracle.c orc_gmres (SciPy's MGS sequence), BJ(8) inverse")
+        else:
+            ip, ix, d = twin.generate(p)
+            A = twin.scipy_csr(ip, ix, d, p.n)
+            b = twin.rhs(p.n)
+            inv = twin.bj_inverse_numpy(ip, ix, d, p.n, 8)
+            s = twin.scipy_gmres(A, b, inv, rtol=1e-8)
+            summ = solve_summary(s.x, s.info, s.inner_iters, s.true_resid, s.b_norm,
+                                 source="scipy.sparse.linalg.gmres, M = BJ(8) LinearOperator (numpy inverses)",
+                                 seconds=round(s.seconds, 1))
+        print(name, "gmres", round(time.time() - t, 1), "s", summ["info"], summ["inner_iters"], flush=True)
+        res.setdefault(name, {})["gmres_bj8"] = summ
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+    print("wrote", out)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gmres-large", nargs="+", default=None, metavar="CFG",
+                    help="only the full-size GMRES summaries of these configs (C2 C3 C4)")
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--skip-small", action="store_true")
     ap.add_argument("--line-only", action="store_true", help="only the line-Jacobi fixtures")
     a = ap.parse_args()
+    if a.gmres_large:
+        gmres_large(os.path.join(HERE, "golden_large.json"), a.gmres_large)
+        sys.exit(0)
     if a.line_only:
         line(os.path.join(HERE, "golden_line.npz"), os.path.join(HERE, "golden_large.json"))
         sys.exit(0)

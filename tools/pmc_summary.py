@@ -19,18 +19,20 @@ live HIP-event avg_us.
 import argparse
 import collections
 import csv
+import hashlib
 import json
 import os
+import re
 import shutil
 import statistics
 
-CLASSES = {   # bench/profile class -> demangled-name prefix in rocprofv3 output (default path:
-              # SELL-64 layout, tridiagonal-factor BJ(8), DCGS2)
-    "spmv_bj_dc": "void vtk::k_sell<double, false, 4, 8, true,",
-    "spmv": "void vtk::k_sell<double, false, 0, 1, false,",
-    "spmv_resid_bj": "void vtk::k_sell<double, false, 3, 8, true,",
-    "spmv_csr": "void vtk::k_spmv<double, false, 0, 1",
-    "spmv_bj_dc_csr": "void vtk::k_spmv<double, false, 4, 8",
+CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv3 output (default
+              # path: SELL-64 layout, tridiagonal-factor BJ(8), DCGS2; fp64 or fp32 values)
+    "spmv_bj_dc": r"void vtk::k_sell<(double|float), false, 4, 8, true,",
+    "spmv": r"void vtk::k_sell<(double|float), false, 0, 1, false,",
+    "spmv_resid_bj": r"void vtk::k_sell<(double|float), false, 3, 8, true,",
+    "spmv_csr": r"void vtk::k_spmv<(double|float), false, 0, 1",
+    "spmv_bj_dc_csr": r"void vtk::k_spmv<(double|float), false, 4, 8",
     "dc_dots": "void vtk::k_dc_dots_rows<",
     "line_apply": "void vtk::k_line_apply<",
     "dc_update": "void vtk::k_dc_update<",
@@ -66,6 +68,11 @@ def main():
     ap.add_argument("--round", required=True)
     ap.add_argument("--src", default="gpurun_out")
     ap.add_argument("--note", default="")
+    ap.add_argument("--tag", default="", help="file-name tag after the round (e.g. c4)")
+    ap.add_argument("--prof", default="prof")
+    ap.add_argument("--fetch", default="pmc_fetch")
+    ap.add_argument("--write", default="pmc_write")
+    ap.add_argument("--cmd", default="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5")
     ap.add_argument("--patch-bench", default=None,
                     help="bench JSON (one line) of the same call whose roofline traffic fields are refreshed "
                          "from this summary (the bench ran before the PMC passes)")
@@ -74,21 +81,25 @@ def main():
     prof = os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
     src = os.path.join(root, a.src)
-    ks = os.path.join(src, "prof", "run_kernel_stats.csv")
+    tag = f"{a.round}_{a.tag}_" if a.tag else f"{a.round}_"
+    ks = os.path.join(src, a.prof, "run_kernel_stats.csv")
     if os.path.exists(ks):
-        shutil.copy(ks, os.path.join(prof, f"{a.round}_kernel_stats.csv"))
-    durations = trace_durations(os.path.join(src, "prof", "run_kernel_trace.csv"))
-    fetch = load(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
-    write = load(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+        shutil.copy(ks, os.path.join(prof, f"{tag}kernel_stats.csv"))
+    durations = trace_durations(os.path.join(src, a.prof, "run_kernel_trace.csv"))
+    fetch = load(os.path.join(src, a.fetch, "run_counter_collection.csv"))
+    write = load(os.path.join(src, a.write, "run_counter_collection.csv"))
+    with open(os.path.join(root, "vt-precondition_amd", "csrc", "vtk_kernels.hip"), "rb") as f:
+        ksha = hashlib.sha256(f.read()).hexdigest()[:16]
     out = {"_how": ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                    "'python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5'; "
+                    f"'{a.cmd}'; "
                     "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
                     "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)"),
-           "note": a.note, "kernels": {}, "durations_us": {}}
+           "note": a.note, "kernels_sha16": ksha, "kernels": {}, "durations_us": {}}
     for cls, prefix in CLASSES.items():
-        fk = [v for k, vs in fetch.items() if k.startswith(prefix) for v in vs]
-        wk = [v for k, vs in write.items() if k.startswith(prefix) for v in vs]
-        dur = [v for k, vs in durations.items() if k.startswith(prefix) for v in vs]
+        rx = re.compile(prefix if prefix.startswith("void") else re.escape(prefix))
+        fk = [v for k, vs in fetch.items() if rx.match(k) for v in vs]
+        wk = [v for k, vs in write.items() if rx.match(k) for v in vs]
+        dur = [v for k, vs in durations.items() if rx.match(k) for v in vs]
         if dur:
             # kernels enqueued past a cycle's stop column return at entry (a few us); the
             # bench's live HIP-event average counts only the working launches
@@ -102,7 +113,7 @@ def main():
         f_kib, w_kib = statistics.mean(fk), statistics.mean(wk) if wk else 0.0
         out["kernels"][cls] = {"dispatches": len(fk), "fetch_kib": f_kib, "write_kib": w_kib,
                                "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024}
-    dst = os.path.join(prof, f"{a.round}_pmc_traffic.json")
+    dst = os.path.join(prof, f"{tag}pmc_traffic.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", dst)

@@ -1090,6 +1090,13 @@ int vtk_comm_info(vtk_ctx *c, int *rank, int *world) {
     return VTK_OK;
 }
 
+int vtk_comm_rccl_count(vtk_ctx *c, int *count) {
+    if (!c || !count) return VTK_ERR_ARG;
+    *count = 0;
+    if (c->comm) NCCLCHK(c, ncclCommCount(c->comm, count));
+    return VTK_OK;
+}
+
 int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t nnz,
                    const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
                    int kind, vtk_csr **out) {

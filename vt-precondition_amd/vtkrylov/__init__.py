@@ -103,6 +103,12 @@ class Context:
         check(lib().vtk_comm_init(self._h, rank, world, buf), self._h)
         self.rank, self.world = rank, world
 
+    def rccl_ranks(self) -> int:
+        """Ranks of the RCCL communicator (ncclCommCount); 0 without one."""
+        n = C.c_int()
+        check(lib().vtk_comm_rccl_count(self._h, C.byref(n)), self._h)
+        return n.value
+
     @staticmethod
     def unique_id() -> bytes:
         buf = C.create_string_buffer(128)

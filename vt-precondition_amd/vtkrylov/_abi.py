@@ -69,6 +69,7 @@ PROTOTYPES = {
     "vtk_comm_unique_id": (C.c_int, [P]),
     "vtk_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
     "vtk_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "vtk_comm_rccl_count": (C.c_int, [P, C.POINTER(C.c_int)]),
     # vtk_comm_init_host: prototype registered by vtkrylov/comm.py (needs the hook struct)
     "vtk_comm_init_host": (C.c_int, [P, C.c_int, C.c_int, P]),
     "vtk_csr_create": (C.c_int, [P, C.c_int64, P, C.c_int64, P, P, P, C.c_int, C.c_int, C.POINTER(P)]),
