@@ -342,7 +342,8 @@ def main():
     ctx.profile(False)
     tot_s = sum(v["seconds"] for v in kprof.values()) or 1.0
     dom = max(kprof, key=lambda k: kprof[k]["seconds"])
-    traffic = pmc_traffic(dom, args.config, world)
+    traffic, traffic_src = pmc_traffic(dom, args.config, world)
+    traffic_spmv, traffic_spmv_src = pmc_traffic("spmv", args.config, world)
     dk = kprof[dom]
 
     # ---- the same solve with the line-implicit x preconditioner, outside the
@@ -408,12 +409,14 @@ def main():
                  "device_read_gbs": read_gbs, "frac_of_read": spmv_gbs / read_gbs},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": dk["gbs"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": dk["gbs"] / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],
                      "avg_us": dk["avg_us"], "launches": dk["launches"],
                      "share_of_solve": dk["seconds"] / tot_s},
         "roofline_spmv": {"kernel": f"spmv ({linfo['layout']}, vtk_spmv)", "bound": "hbm",
                           "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": spmv_gbs / HBM_PEAK_GBS, "traffic": pmc_traffic("spmv", args.config, world),
+                          "frac": spmv_gbs / HBM_PEAK_GBS, "traffic": traffic_spmv,
+                          "traffic_source": traffic_spmv_src,
                           "algorithmic_bytes_per_launch": B},
         "kernels": {k: {"avg_us": round(v["avg_us"], 2), "gbs": round(v["gbs"], 1),
                         "launches": v["launches"], "share": round(v["seconds"] / tot_s, 4)}
@@ -435,19 +438,40 @@ def main():
         dist.destroy_process_group()
 
 
+def kernels_sha16():
+    import hashlib
+    with open(os.path.join(ROOT, "vt-precondition_amd", "csrc", "vtk_kernels.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def pmc_traffic(cls, config, world):
-    """HBM bytes per launch of kernel class `cls` from the newest committed rocprofv3 PMC
-    summary (profiles/rNN_pmc_traffic.json, tools/pmc_summary.py) of this same command
-    (C3, one GPU); None when no summary matches."""
+    """(HBM bytes per launch of kernel class `cls`, source) from the newest committed rocprofv3
+    PMC summary (profiles/rNN[_tag]_pmc_traffic.json, tools/pmc_summary.py) taken on the same
+    config at one GPU AND on the same kernel source (its `kernels_sha16` must equal the hash of
+    the vtk_kernels.hip being benched).  (None, why) otherwise: a summary of other kernels is
+    never reported as this run's traffic."""
     import glob
-    if config != "C3" or world != 1:
-        return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        k = json.load(f)["kernels"].get(cls)
-    return None if k is None else k["hbm_bytes_per_launch"]
+    import re
+    if world != 1:
+        return None, "no PMC summary for multi-GPU runs"
+    sha = kernels_sha16()
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True)
+    stale = None
+    for path in files:
+        with open(path) as f:
+            rec = json.load(f)
+        m = re.match(r"r\d+_(c\d)_pmc_traffic\.json$", os.path.basename(path))
+        cfg = rec.get("config") or (m.group(1).upper() if m else "C3")
+        if cfg != config:
+            continue
+        if rec.get("kernels_sha16") != sha:
+            stale = stale or os.path.basename(path)
+            continue
+        k = rec["kernels"].get(cls)
+        if k is not None:
+            return k["hbm_bytes_per_launch"], f"{os.path.basename(path)} (kernels {sha})"
+    return None, (f"newest {config} summary {stale} profiles other kernel sources than {sha}" if stale
+                  else f"no {config} PMC summary")
 
 
 def params_nnz(dim, shape):

@@ -1,0 +1,78 @@
+"""Full-size parity pins at the headline configs (VERDICT r1 "next" 2): the bench's own path
+(DCGS2 + tridiagonal-factor BJ(8) + SELL, the defaults) and SciPy's sequence (MGS + the
+bit-exact inverse BJ apply) against SciPy's GMRES(20) + BJ(8) run to rtol 1e-8 at C2 (5M rows)
+and C3 (20M rows, the bench workload), and C4 (50M rows, fp32 values) against the C oracle's
+SciPy-sequence solve.  Summaries: tests/golden/golden_large.json, written by
+tests/golden/make_golden.py --gmres-large (iterative.py:582-841).
+
+Bars: info equal; inner iterations within +-1; ||x||_2 relative 1e-9; x[:8], x[-8:] and 64
+entries at a fixed stride within 1e-8 of max|x_ref| when the iteration counts agree (1e-6 when
+they differ by one: the solutions then differ by one Arnoldi step's correction, itself below
+rtol); the true residual ||b - A x|| recomputed on the host by the oracle SpMV <= 1e-8 ||b||.
+"""
+import numpy as np
+import pytest
+
+from oracle import coracle, twin
+
+pytestmark = pytest.mark.gpu
+
+PATHS = {   # name -> (orth, bj mode)
+    "default": ("auto", "auto"),          # what bench.py measures: DCGS2 + tridiag + SELL
+    "scipy_sequence": ("mgs", "inverse"),
+}
+
+
+def _solve(vk, gpu, name, path):
+    p = twin.CONFIGS[name]
+    A = vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=gpu)
+    orth, mode = PATHS[path]
+    M = vk.block_jacobi(A, 8, mode=mode)
+    b = vk.rhs_splitmix(p.n)
+    x, info = vk.gmres(A, b, rtol=1e-8, M=M, orth=None if orth == "auto" else orth)
+    st = vk.last_stats()
+    layout = A.layout_info()["layout"]
+    mmode = M.mode
+    ip, ix, d = A.download()
+    M.close()
+    A.close()
+    return p, x, info, st, b, (ip, ix, d), layout, mmode
+
+
+def _check(g, x, info, st, b, csr):
+    assert info == g["info"] == 0
+    assert abs(st.inner_iters - g["inner_iters"]) <= 1, (st.inner_iters, g["inner_iters"])
+    assert np.linalg.norm(x) == pytest.approx(g["x_norm2"], rel=1e-9)
+    scale = max(np.max(np.abs(g["x_sample"])), np.max(np.abs(g["x_first8"])))
+    tol = (1e-8 if st.inner_iters == g["inner_iters"] else 1e-6) * scale
+    np.testing.assert_allclose(x[:8], g["x_first8"], rtol=0, atol=tol)
+    np.testing.assert_allclose(x[-8:], g["x_last8"], rtol=0, atol=tol)
+    s = g["x_sample_stride"]
+    np.testing.assert_allclose(x[::s][:64], g["x_sample"], rtol=0, atol=tol)
+    ip, ix, d = csr
+    res = np.linalg.norm(b - coracle.spmv(ip, ix, d, x))
+    assert res <= 1e-8 * g["b_norm2"]
+    assert st.rnorm == pytest.approx(res, rel=1e-6)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("path", sorted(PATHS))
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_gmres_full_size_vs_scipy(gpu, vk_lib, golden_large, name, path):
+    p, x, info, st, b, csr, layout, mmode = _solve(vk_lib, gpu, name, path)
+    if path == "default":   # the bench's configuration, not a fallback
+        assert layout == "sell" and mmode == "tridiag" and st.orth == 1
+    else:
+        assert mmode == "inverse" and st.orth == 0
+    _check(golden_large[name]["gmres_bj8"], x, info, st, b, csr)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("path", sorted(PATHS))
+def test_gmres_c4_vs_oracle(gpu, vk_lib, golden_large, path):
+    g = golden_large["C4"].get("gmres_bj8")
+    if g is None:
+        pytest.fail("golden_large.json has no C4 summary (make_golden.py --gmres-large C4)")
+    p, x, info, st, b, csr, layout, mmode = _solve(vk_lib, gpu, "C4", path)
+    assert layout == "sell"
+    _check(g, x, info, st, b, csr)

@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--fetch", default="pmc_fetch")
     ap.add_argument("--write", default="pmc_write")
     ap.add_argument("--cmd", default="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5")
+    ap.add_argument("--config", default="C3", help="bench config the profiled command ran (bench.py matches it)")
     ap.add_argument("--patch-bench", default=None,
                     help="bench JSON (one line) of the same call whose roofline traffic fields are refreshed "
                          "from this summary (the bench ran before the PMC passes)")
@@ -94,7 +95,7 @@ def main():
                     f"'{a.cmd}'; "
                     "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
                     "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)"),
-           "note": a.note, "kernels_sha16": ksha, "kernels": {}, "durations_us": {}}
+           "note": a.note, "config": a.config, "kernels_sha16": ksha, "kernels": {}, "durations_us": {}}
     for cls, prefix in CLASSES.items():
         rx = re.compile(prefix if prefix.startswith("void") else re.escape(prefix))
         fk = [v for k, vs in fetch.items() if rx.match(k) for v in vs]

@@ -444,6 +444,24 @@ int build_sell(vtk_csr *A, bool only_if_compact, bool *built) {
     if (e == hipSuccess) e = hipMemcpyAsync(&sl.entries, sl.d_off + nch, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) { drop(); return fail(c, VTK_ERR_HIP, std::string("SELL build: ") + hipGetErrorString(e)); }
+    // nearly uniform widths (the 4D operator: a few chunks of 64 velocity-boundary rows are one
+    // entry narrower) are padded to the widest chunk when that costs <= 2 % more entries: every
+    // chunk's offset is then 64 W q and the kernels take the compile-time-width path (no offset
+    // loads at the head of each chunk)
+    if (nch > 0 && std::getenv("VTK_SELL_NOPAD") == nullptr) {
+        std::vector<int64_t> off((size_t)nch + 1);
+        e = hipMemcpy(off.data(), sl.d_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { drop(); return fail(c, VTK_ERR_HIP, std::string("SELL build: ") + hipGetErrorString(e)); }
+        int64_t wmax = 0;
+        for (int64_t q = 0; q < nch; ++q) wmax = std::max(wmax, (off[(size_t)q + 1] - off[(size_t)q]) >> 6);
+        const int64_t uni = nch * 64 * wmax;
+        if (wmax > 0 && uni != sl.entries && (double)uni <= 1.02 * (double)sl.entries) {
+            for (int64_t q = 0; q <= nch; ++q) off[(size_t)q] = 64 * wmax * q;
+            e = hipMemcpy(sl.d_off, off.data(), off.size() * sizeof(int64_t), hipMemcpyHostToDevice);
+            if (e != hipSuccess) { drop(); return fail(c, VTK_ERR_HIP, std::string("SELL build: ") + hipGetErrorString(e)); }
+            sl.entries = uni;
+        }
+    }
     if (only_if_compact && (double)sl.entries > 1.25 * (double)A->nnz + 64.0) { drop(); return VTK_OK; }
     const size_t vb = A->fp32 ? 4 : 8;
     e = hipMalloc(&sl.d_col, (size_t)std::max<int64_t>(sl.entries, 1) * 4);

@@ -14,6 +14,8 @@
 
 #include <float.h>
 
+#include <cstdlib>
+
 #include "vtk_internal.hpp"
 #include "vtk_vlasov.hpp"
 
@@ -607,15 +609,38 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #ifndef VTK_SELL_SWZ
 #define VTK_SELL_SWZ 0   // XCD-aware group order (xcd_swizzle)
 #endif
+// compile-time chunk width of the uniform-width SELL copies the stencil operators produce (2D
+// Vlasov: 5, 4D: 9); 0 = the runtime-width loop
+#ifndef VTK_SELL_WU
+#define VTK_SELL_WU 1
+#endif
+#ifndef VTK_DC_JB9
+#define VTK_DC_JB9 VTK_DC_JB
+#endif
+#ifndef VTK_DC_VPRE9
+#define VTK_DC_VPRE9 0   // C4 fused step: 1577 -> 1392 us without the early basis batch (spill 72 -> 20 B)
+#endif
+#ifndef VTK_DC_PSW9
+#define VTK_DC_PSW9 9   // DC load batch at width 9 (C4)
+#endif
+#ifndef VTK_GATHER_UNCOND
+#define VTK_GATHER_UNCOND 1
+#endif
 #ifndef VTK_SELL_WPE
 #define VTK_SELL_WPE 4   // minimum waves/SIMD the SELL kernels are register-limited to
 #endif
-template <typename VT, bool HALO, int EPI, int BS, bool TRI = false, int PSWT = 0>
+// WU > 0: every chunk is WU entries wide (Sell::uniform_w == WU, checked by the launch): the
+// chunk's code words are all issued with its dictionary and the entry loop has compile-time
+// bounds, so a row wider than one code word (C4: 9 entries) costs no extra dependent round trip
+// for its second word and no batch boundary at the word edge.
+template <typename VT, bool HALO, int EPI, int BS, bool TRI = false, int PSWT = 0, int WU = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE))) void k_sell(SpmvK<VT, HALO> a) {
-    // entries per load batch (DC: registers; PSWT: a row length the launch picked)
-    constexpr int PSW = EPI == EPI_PREC_DC ? (PSWT > 0 ? PSWT : VTK_DC_PSW) : 8;
+    // entries per load batch (DC: registers; PSWT: a row length the launch picked; WU without
+    // PSWT: the whole row in one batch)
+    constexpr int PSW = PSWT > 0 ? PSWT : (WU > 0 ? WU : (EPI == EPI_PREC_DC ? VTK_DC_PSW : 8));
     constexpr int KB = VTK_DC_KB;   // basis vectors per load batch (DC)
-    constexpr int JB = VTK_DC_JB;   // basis vectors with per-lane register accumulators (DC)
+    // basis vectors with per-lane register accumulators (DC; the 9-wide rows hold more operands)
+    constexpr int JB = WU > 8 ? VTK_DC_JB9 : VTK_DC_JB;
     constexpr bool DC = EPI == EPI_PREC_DC;
     constexpr bool HOIST = DC && VTK_DC_HOIST;
     constexpr bool HOISTE = !DC && EPI != EPI_PLAIN && VTK_EPI_HOIST;   // the other epilogues
@@ -661,34 +686,93 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         }
         // VPRE: the first batch of basis rows is loaded before the SpMV (no dependence on it),
         // in flight during the gather chain
-        [[maybe_unused]] double vpre[(DC && VTK_DC_VPRE) ? KB : 1];
-        if constexpr (DC && VTK_DC_VPRE) {
+        constexpr bool VPRE = DC && VTK_DC_VPRE && (WU <= 8 || VTK_DC_VPRE9);
+        [[maybe_unused]] double vpre[VPRE ? KB : 1];
+        if constexpr (VPRE) {
 #pragma unroll
             for (int u = 0; u < KB; ++u)
                 vpre[u] = (u < JB && u < a.j && act) ? __builtin_nontemporal_load(a.V + row + (size_t)u * a.ld) : 0.0;
         }
-        if (64 * q < a.n_local) {
+        // products of one batch, summed serially in stored order (padding skipped)
+        auto batch = [&](const auto &c, const auto &d) {
+            constexpr int NB = sizeof(c) / sizeof(c[0]);
+            double xv[NB];
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                // UNCOND: padding slots gather the lane's own x[row] (the line of its diagonal
+                // entry) instead of branching around the load: the gathers issue back to back
+                // with no exec-mask blocks.  (x[0] for every padding slot measured 1.6x slower on
+                // C4: one hot L2 line for the whole chip.)
+                if constexpr (VTK_GATHER_UNCOND) xv[u] = xload(a, c[u] >= 0 ? c[u] : (act ? row : 0));
+                else xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < NB; ++u)
+                if (c[u] >= 0) s += d[u] * xv[u];
+            if constexpr (TRIM) {
+#pragma unroll
+                for (int u = 0; u < NB; ++u) {
+                    if (c[u] == row - 1 && ii > 0) sub = sub + d[u];
+                    if (c[u] == row + 1 && ii < BS - 1) sup = sup + d[u];
+                }
+            }
+        };
+        if constexpr (WU > 0) {
+            if (64 * q < a.n_local) {
+                constexpr int NWD = (WU + 7) / 8;   // 4-bit code words per lane
+                const int64_t o0 = (int64_t)q * 64 * WU;
+                const VT *vv = a.sell_val + o0 + lane;
+                uint32_t wd[NWD];
+                int dv = 0;
+                bool wide = true;   // wave-uniform
+                if (a.pk) {
+                    const uint32_t *pw = a.pk + (int64_t)q * 64 * NWD + lane;
+#pragma unroll
+                    for (int u = 0; u < NWD; ++u) wd[u] = __builtin_nontemporal_load(pw + u * 64);
+                    dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
+                }
+                // the row's values do not depend on the column form: issued with the codes and the
+                // dictionary, before the form test waits for the dictionary
+                VT dall[WU];   // raw (fp32 values: one VGPR each until used)
+#pragma unroll
+                for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
+                if (a.pk) wide = __shfl(dv, 15, 64) != 0;
+                // one copy of the unrolled entry loop per column form (no branch inside it)
+                auto entries = [&](auto wide_c) {
+                    constexpr bool WIDE = decltype(wide_c)::value;
+                    const int32_t *cc = a.sell_col + o0 + lane;
+#pragma unroll
+                    for (int k0 = 0; k0 < WU; k0 += PSW) {
+                        int c[PSW];
+                        double d[PSW];
+#pragma unroll
+                        for (int u = 0; u < PSW; ++u) {
+                            const int k = k0 + u;
+                            if (k >= WU) {
+                                c[u] = -1;
+                                d[u] = 0.0;
+                                continue;
+                            }
+                            if constexpr (WIDE) {
+                                c[u] = __builtin_nontemporal_load(cc + k * 64);
+                            } else {
+                                const int code = (int)((wd[k >> 3] >> (4 * (k & 7))) & 15u);
+                                const int off = __shfl(dv, code, 64);
+                                c[u] = code != PK_CODES ? row + off : -1;
+                            }
+                            d[u] = (double)dall[k];
+                        }
+                        batch(c, d);
+                    }
+                };
+                if (wide) entries(std::true_type{});
+                else entries(std::false_type{});
+            }
+        } else if (64 * q < a.n_local) {
             // uniform widths: offsets from q (no scalar loads ahead of the value / code loads)
             const int64_t o0 = a.sell_uw ? (int64_t)q * 64 * a.sell_uw : a.sell_off[q];
             const int w = a.sell_uw ? a.sell_uw : (int)((a.sell_off[q + 1] - o0) >> 6);
             const VT *vv = a.sell_val + o0 + lane;
-            // products of one batch, summed serially in stored order (padding skipped)
-            auto batch = [&](const auto &c, const auto &d) {
-                constexpr int NB = sizeof(c) / sizeof(c[0]);
-                double xv[NB];
-#pragma unroll
-                for (int u = 0; u < NB; ++u) xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
-#pragma unroll
-                for (int u = 0; u < NB; ++u)
-                    if (c[u] >= 0) s += d[u] * xv[u];
-                if constexpr (TRIM) {
-#pragma unroll
-                    for (int u = 0; u < NB; ++u) {
-                        if (c[u] == row - 1 && ii > 0) sub = sub + d[u];
-                        if (c[u] == row + 1 && ii < BS - 1) sup = sup + d[u];
-                    }
-                }
-            };
             // columns: dictionary codes (one 32-bit word per 8 entries of a lane), or int32
             // for "wide" chunks / unpacked copies; wave-uniform choice, one code path
             bool wide = true;
@@ -750,7 +834,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 double v[KB];
 #pragma unroll
                 for (int u = 0; u < KB; ++u) {
-                    if constexpr (VTK_DC_VPRE) {
+                    if constexpr (VPRE) {
                         if (k0 == 0) {
                             v[u] = vpre[u];
                             continue;
@@ -968,6 +1052,26 @@ size_t sell_scan_bytes(int64_t n) {
         else hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_, BS_, TRI_>), g, blk, 0, s, a);          \
     } while (0)
 
+// workgroups of the plain SELL SpMV (no partials: free of GMAX); VTK_PLAIN_GRID for tuning
+static inline int plain_grid() {
+    static const int g = [] {
+        const char *e = std::getenv("VTK_PLAIN_GRID");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 2 * GMAX;
+    }();
+    return g;
+}
+static inline int sell_wu(const SpmvIn &in) {
+    if (!VTK_SELL_WU || !VTK_SELL_UNIFORM || !in.sell || !in.groups) return 0;
+    const int w = in.sell->uniform_w;
+    return (w == 5 || w == 9) ? w : 0;
+}
+// the plain SpMV takes the compile-time path only for rows wider than one code word (C4 plain
+// 848 -> 698 us); at width 5 the runtime loop is faster (C3 220 vs 233 us)
+static inline int sell_wu_plain(const SpmvIn &in) {
+    const int w = sell_wu(in);
+    return w > 8 ? w : 0;
+}
+
 template <typename VT, bool HALO, int EPI, int MAXBS>
 static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, bool sell, dim3 g, hipStream_t s) {
     const dim3 blk(NT);
@@ -1025,8 +1129,10 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
     if (epi == EPI_PLAIN) {
         // no partials: SELL fills the chip at its 8 waves/SIMD (52 VGPRs) with 2048 workgroups
         // (tools/probe_sell.hip, C4: 965 us at 2048 vs 1362 us at 1024; C3 within 2 %)
-        const dim3 gp(sell ? (unsigned)std::max(1, std::min(in.groups->count, 2 * GMAX)) : g.x);
-        if (sell) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false>), gp, blk, 0, s, a);
+        const dim3 gp(sell ? (unsigned)std::max(1, std::min(in.groups->count, plain_grid())) : g.x);
+        const int wu = sell_wu_plain(in);
+        if (sell && wu == 9) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false, 0, 9>), gp, blk, 0, s, a);
+        else if (sell) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false>), gp, blk, 0, s, a);
         else hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1, false>), g, blk, 0, s, a);
         return hipGetLastError();
     }
@@ -1053,6 +1159,15 @@ static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, 
     // batch of 5 covers a row (C3 fused step 621 -> 590 us); wider rows keep batches of 4 (C4:
     // 5 would cost +5 %)
     const bool sell = in.sell && in.groups;
+    const int wu = sell_wu(in);
+    if (sell && bj.tri && bs == 8 && wu == 5) {
+        hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, 5, 5>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        return hipGetLastError();
+    }
+    if (sell && bj.tri && bs == 8 && wu == 9) {
+        hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, VTK_DC_PSW9, 9>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        return hipGetLastError();
+    }
     if (sell && bj.tri && bs == 8 && in.sell->nch > 0 && in.sell->entries <= in.sell->nch * 64 * 5) {
         hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, 5>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
         return hipGetLastError();

@@ -503,13 +503,21 @@ def last_stats() -> SolveStats | None:
 def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=None,
           callback=None, callback_type=None, orth=None):
     """``scipy.sparse.linalg.gmres`` on the GPU (iterative.py:582-841, left-preconditioned
-    restarted GMRES with modified Gram-Schmidt).  Returns ``(x, info)``.
+    restarted GMRES: SciPy's control flow, ptol schedule, ``dlartg`` Givens rotations and
+    ``info`` convention).  Returns ``(x, info)``.
+
+    Orthogonalisation: the DEFAULT (``orth=None``/``"auto"`` with the context left at auto) is
+    DCGS2 -- delayed classical Gram-Schmidt with re-orthogonalisation, one global reduction per
+    Arnoldi step -- whenever ``restart <= 32``, else MGS.  DCGS2 builds the same Krylov basis in
+    exact arithmetic but not SciPy's floating-point sequence: info matches and the inner
+    iteration count may differ by one.  ``orth="mgs"`` runs SciPy's exact
+    modified Gram-Schmidt sequence (iterative.py:755-759); ``orth="dcgs2"`` forces DCGS2.
 
     ``A``: a :class:`CsrOperator` or any SciPy sparse matrix (uploaded).  ``M``: None, a
     :class:`BlockJacobi` or a :class:`LineJacobi` built on ``A``; any other preconditioner raises TypeError (no CPU
     fallback).  ``callback`` is not supported (the Arnoldi loop never returns to the host).
-    ``orth`` (extension): "mgs" (SciPy's exact sequence), "dcgs2" (one reduction per step,
-    restart <= 32) or "auto"/None (the context's setting; default DCGS2 when restart <= 32).
+    ``restart``/``maxiter``: None = SciPy's defaults (20 / 10 n); explicit values must be
+    positive integers (ValueError otherwise).
     """
     global _last_stats
     if callback is not None:
@@ -522,6 +530,9 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     if atol == "legacy" or atol is None or atol < 0:
         raise ValueError(f"'scipy.sparse.linalg.gmres' called with invalid `atol`={atol}; "
                          "if set, `atol` must be a real, non-negative number.")
+    for name, v in (("restart", restart), ("maxiter", maxiter)):
+        if v is not None and (int(v) != v or int(v) <= 0):
+            raise ValueError(f"vtkrylov.gmres: {name} must be a positive integer or None, got {v!r}")
     n = A.n_local
     vb = _Vec(b, n)
     if x0 is None:
