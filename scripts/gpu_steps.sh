@@ -55,6 +55,11 @@ for s in "$@"; do
         pmcfc4) step pmcfc4 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_c4 -o run --output-format csv -- python bench.py --config C4 --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 3 ;;
         pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
         pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
+        profsolo) step profsolo 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsolo -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --comm-solo --spmv-reps 5 ;;
+        profsoloc2) step profsoloc2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsoloc2 -o run --output-format csv -- python bench.py --config C2 --steps 2 --warmup 1 --no-cpu-baseline --comm-solo --spmv-reps 5 ;;
+        profc2) step profc2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc2 -o run --output-format csv -- python bench.py --config C2 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
+        evab) for E in 1 2 4 1 2 4; do VTK_EV_EVERY=$E step evab_c2_$E 300 python bench.py --config C2 --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; python tools/bench_brief.py gpurun_out/evab_c2_$E.log; VTK_EV_EVERY=$E step evab_solo_$E 300 python bench.py --config C2 --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 5 --comm-solo || exit $?; python tools/bench_brief.py gpurun_out/evab_solo_$E.log; done ;;
+        large) step large 600 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -49,4 +49,7 @@ def test_rccl_solo_gmres(vk_lib, solo, layout, orth):
     assert np.linalg.norm(xs - ref.x) / np.linalg.norm(ref.x) <= 1e-9
     assert "allreduce" in prof and prof["allreduce"]["launches"] > 0   # the RCCL path ran
     if orth == "dcgs2":
-        assert "dc_finalize" in prof and "spmv_bj_dc_bd" in prof       # split launches + finalize
+        # the distributed step (interior launch + finalize + all-reduce); one rank has no halo
+        # and no boundary rows, so no exchange and no boundary launch
+        assert "dc_finalize" in prof and "spmv_bj_dc" in prof
+        assert "spmv_bj_dc_bd" not in prof and "halo" not in prof

@@ -709,6 +709,13 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         return VTK_OK;
     };
     bool broke = false;
+    static const int ev_every = [] {
+        const char *e = std::getenv("VTK_EV_EVERY");
+        const int v = e ? std::atoi(e) : 1;
+        return v >= 1 && v <= LOOKAHEAD + 1 ? v : 1;
+    }();
+    int ev_step[LOOKAHEAD + 1];
+    int nev = 0, synced = 0;
     for (int j = 0; j < m; ++j) {
         double *pj = s.V + (size_t)j * s.ld;
         int cnt = 0;
@@ -720,18 +727,25 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             in.halo = nullptr;   // interior tiles read owned columns only
             const double f_in = (s.A->use_sell ? s.A->g_in.count * 256.0 : (double)s.M->tiles_in.nrows) /
                                 std::max<double>(1.0, (double)n);
-            TRY(halo_exchange_async(s.A, pj));
+            // a rank with no x-neighbour data to send or receive (one rank) skips the exchange
+            // and its event hand-offs; one without boundary rows skips the boundary launch
+            const bool exch = s.A->n_send > 0 || s.A->n_halo > 0;
+            const bool has_bd = s.A->use_sell ? s.A->g_bd.count > 0 : s.M->tiles_bd.ntiles > 0;
+            if (exch) TRY(halo_exchange_async(s.A, pj));
             {
                 Prof pf(c, "spmv_bj_dc", j, b_step * std::min(1.0, f_in));
                 HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             }
-            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-            {
+            // the all-reduce below stays behind this rank's exchange on every rank (one order
+            // of RCCL operations on the communicator)
+            if (exch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+            cnt = spmv_grid(in);
+            if (has_bd) {
                 Prof pf(c, "spmv_bj_dc_bd", j, b_step * std::max(0.0, 1.0 - f_in));
                 HIPCHK(c, launch_spmv_dc(bd, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart + spmv_grid(in), stop, j,
                                          c->stream));
+                cnt += spmv_grid(bd);
             }
-            cnt = spmv_grid(in) + spmv_grid(bd);
         } else if (fused) {
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
@@ -745,12 +759,22 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         TRY(reduce_step(j, s.w, j, cnt));
         { Prof pf(c, "dc_update", j, n8 * (j + 4));
           HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, fused ? 0 : 1, c->stream)); }
-        HIPCHK(c, hipEventRecord(ev[j % (LOOKAHEAD + 1)], c->stream));
-        if (j >= LOOKAHEAD) {
-            HIPCHK(c, hipEventSynchronize(ev[(j - LOOKAHEAD) % (LOOKAHEAD + 1)]));
-            // column cc stops in step cc (early commit) or cc+1: act only once every rank ran it
-            if (*mirror <= j - LOOKAHEAD - 1) { broke = true; break; }
+        // throttle: an event every EV_EVERY steps (each record costs the stream a few us); the
+        // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
+        // has passed there.  Column cc stops in step cc (early commit) or cc+1: act only once
+        // every rank ran it.
+        if ((j + 1) % ev_every == 0) {
+            HIPCHK(c, hipEventRecord(ev[nev % (LOOKAHEAD + 1)], c->stream));
+            ev_step[nev % (LOOKAHEAD + 1)] = j;
+            ++nev;
         }
+        while (synced < nev && ev_step[synced % (LOOKAHEAD + 1)] <= j - LOOKAHEAD) {
+            const int js = ev_step[synced % (LOOKAHEAD + 1)];
+            HIPCHK(c, hipEventSynchronize(ev[synced % (LOOKAHEAD + 1)]));
+            ++synced;
+            if (*mirror <= js - 1) { broke = true; break; }
+        }
+        if (broke) break;
     }
     if (!broke) TRY(reduce_step(m, nullptr, m, 0));   // closing: only if column m-1 is still open
     return VTK_OK;
