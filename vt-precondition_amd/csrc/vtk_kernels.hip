@@ -604,7 +604,7 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #define VTK_WORD_EARLY 1   // first code word loaded with the dictionary (A/B: fused -1 %, residual -6 %)
 #endif
 #ifndef VTK_DC_VPRE
-#define VTK_DC_VPRE 1   // first basis batch loaded ahead of the SpMV (DC; A/B: -0.3 %..-0.6 % time)
+#define VTK_DC_VPRE 0   // first basis batch loaded ahead of the SpMV (r01: -0.3 %..-0.6 % time; with the compile-time-width path +1 %: off)
 #endif
 #ifndef VTK_SELL_SWZ
 #define VTK_SELL_SWZ 0   // XCD-aware group order (xcd_swizzle)
@@ -622,6 +622,15 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #endif
 #ifndef VTK_DC_PSW9
 #define VTK_DC_PSW9 9   // DC load batch at width 9 (C4)
+#endif
+#ifndef VTK_SELL_PIPE
+#define VTK_SELL_PIPE 0    // fused DC step, rows <= 8 wide (C3: 536 -> 541 us with it: off)
+#endif
+#ifndef VTK_SELL_PIPE9
+#define VTK_SELL_PIPE9 0   // fused DC step, 9-wide rows (C4: 104 B spill, 1442 -> 1935 us: off)
+#endif
+#ifndef VTK_SELL_PIPEP
+#define VTK_SELL_PIPEP 0   // plain / other epilogues (C4 plain 695 -> 704-712 us with it: off)
 #endif
 #ifndef VTK_GATHER_UNCOND
 #define VTK_GATHER_UNCOND 1
@@ -658,6 +667,41 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         for (int k = 0; k < JB; ++k) { as_[k] = 0.0; az_[k] = 0.0; }
     }
     const int t0 = VTK_SELL_SWZ ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    // PIPE (compile-time widths): the next chunk's code words, dictionary, values and own-row
+    // operands are loaded while this chunk's gathers are in flight -- issued right after them,
+    // so waiting for the gathers does not wait for the prefetch -- and consumed one iteration
+    // later: one dependent memory round trip less per chunk.
+    constexpr bool PIPE = WU > 0 && (DC ? (WU > 8 ? VTK_SELL_PIPE9 : VTK_SELL_PIPE) : VTK_SELL_PIPEP);
+    constexpr int NWDP = WU > 0 ? (WU + 7) / 8 : 1;
+    [[maybe_unused]] VT pf_d[PIPE ? WU : 1];
+    [[maybe_unused]] uint32_t pf_wd[NWDP];
+    [[maybe_unused]] int pf_dv = 0;
+    [[maybe_unused]] double pf_m = 1.0, pf_p = 0.0;
+    auto prefetch = [&](int tt) {
+        if constexpr (PIPE) {
+            if (tt >= a.ngroups) return;   // wave-uniform
+            const int gg = a.group_list ? a.group_list[tt] : tt;
+            const int qq = VTK_SCALAR_Q ? __builtin_amdgcn_readfirstlane(4 * gg + wv) : 4 * gg + wv;
+            const int rr = 64 * qq + lane;
+            if (64 * qq >= a.n_local) return;
+            const VT *vv = a.sell_val + (int64_t)qq * 64 * WU + lane;
+            if (a.pk) {
+                const uint32_t *pw = a.pk + (int64_t)qq * 64 * NWDP + lane;
+#pragma unroll
+                for (int u = 0; u < NWDP; ++u) pf_wd[u] = __builtin_nontemporal_load(pw + u * 64);
+                pf_dv = lane < 16 ? a.dict[(int64_t)qq * 16 + lane] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < WU; ++k) pf_d[k] = __builtin_nontemporal_load(vv + k * 64);
+            if constexpr (HOIST) {
+                if (rr < a.n_local) {
+                    if constexpr (TRI && BS > 0) pf_m = ld_nt<1>(a.tri + a.tri_ld + rr);
+                    pf_p = a.x[rr];
+                }
+            }
+        }
+    };
+    if constexpr (PIPE) prefetch(t0);
     for (int t = t0; t < a.ngroups; t += gridDim.x) {
         const int g = a.group_list ? a.group_list[t] : t;
         const int q = VTK_SCALAR_Q ? __builtin_amdgcn_readfirstlane(4 * g + wv) : 4 * g + wv;
@@ -670,7 +714,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // HOIST: the row's own operands (BJ factor m, p, b, v0) issued ahead of the CSR loads,
         // so the epilogue does not wait a memory round trip per chunk (EPI_PREC: 352 -> ... us)
         double mrow = 1.0, pv = 0.0, bv = 0.0, v0v = 0.0;
-        if constexpr (HOIST) {
+        [[maybe_unused]] VT cur_d[PIPE ? WU : 1];
+        [[maybe_unused]] uint32_t cur_wd[NWDP];
+        [[maybe_unused]] int cur_dv = 0;
+        if constexpr (PIPE) {
+#pragma unroll
+            for (int k = 0; k < WU; ++k) cur_d[k] = pf_d[k];
+#pragma unroll
+            for (int u = 0; u < NWDP; ++u) cur_wd[u] = pf_wd[u];
+            cur_dv = pf_dv;
+            if constexpr (HOIST) {
+                mrow = act ? pf_m : 1.0;
+                pv = act ? pf_p : 0.0;
+            }
+        }
+        if constexpr (HOIST && !PIPE) {
             if (act) {
                 if constexpr (TRIM) mrow = ld_nt<1>(a.tri + a.tri_ld + row);
                 pv = a.x[row];
@@ -694,7 +752,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 vpre[u] = (u < JB && u < a.j && act) ? __builtin_nontemporal_load(a.V + row + (size_t)u * a.ld) : 0.0;
         }
         // products of one batch, summed serially in stored order (padding skipped)
-        auto batch = [&](const auto &c, const auto &d) {
+        auto batch = [&](const auto &c, const auto &d, auto mid) {
             constexpr int NB = sizeof(c) / sizeof(c[0]);
             double xv[NB];
 #pragma unroll
@@ -706,6 +764,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 if constexpr (VTK_GATHER_UNCOND) xv[u] = xload(a, c[u] >= 0 ? c[u] : (act ? row : 0));
                 else xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
             }
+            mid();
 #pragma unroll
             for (int u = 0; u < NB; ++u)
                 if (c[u] >= 0) s += d[u] * xv[u];
@@ -725,17 +784,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 uint32_t wd[NWD];
                 int dv = 0;
                 bool wide = true;   // wave-uniform
-                if (a.pk) {
-                    const uint32_t *pw = a.pk + (int64_t)q * 64 * NWD + lane;
-#pragma unroll
-                    for (int u = 0; u < NWD; ++u) wd[u] = __builtin_nontemporal_load(pw + u * 64);
-                    dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
-                }
-                // the row's values do not depend on the column form: issued with the codes and the
-                // dictionary, before the form test waits for the dictionary
                 VT dall[WU];   // raw (fp32 values: one VGPR each until used)
+                if constexpr (PIPE) {
 #pragma unroll
-                for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
+                    for (int u = 0; u < NWD; ++u) wd[u] = cur_wd[u];
+                    dv = cur_dv;
+#pragma unroll
+                    for (int k = 0; k < WU; ++k) dall[k] = cur_d[k];
+                } else {
+                    if (a.pk) {
+                        const uint32_t *pw = a.pk + (int64_t)q * 64 * NWD + lane;
+#pragma unroll
+                        for (int u = 0; u < NWD; ++u) wd[u] = __builtin_nontemporal_load(pw + u * 64);
+                        dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
+                    }
+                    // the row's values do not depend on the column form: issued with the codes
+                    // and the dictionary, before the form test waits for the dictionary
+#pragma unroll
+                    for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
+                }
                 if (a.pk) wide = __shfl(dv, 15, 64) != 0;
                 // one copy of the unrolled entry loop per column form (no branch inside it)
                 auto entries = [&](auto wide_c) {
@@ -762,7 +829,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                             }
                             d[u] = (double)dall[k];
                         }
-                        batch(c, d);
+                        batch(c, d, [&] {
+                            if constexpr (PIPE) {
+                                if (k0 == 0) {
+                                    __builtin_amdgcn_sched_barrier(0);
+                                    prefetch(t + (int)gridDim.x);
+                                    __builtin_amdgcn_sched_barrier(0);
+                                }
+                            }
+                        });
                     }
                 };
                 if (wide) entries(std::true_type{});
@@ -815,7 +890,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     for (int u = 0; u < PSW; ++u)
                         d[u] = (VTK_VAL_EARLY ? (h + u < 8 && k0 + h + u < w) : c[u] >= 0)
                                    ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
-                    batch(c, d);
+                    batch(c, d, [] {});
                 }
             }
         }
