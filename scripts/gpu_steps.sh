@@ -59,6 +59,11 @@ for s in "$@"; do
         profsoloc2) step profsoloc2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsoloc2 -o run --output-format csv -- python bench.py --config C2 --steps 2 --warmup 1 --no-cpu-baseline --comm-solo --spmv-reps 5 ;;
         profc2) step profc2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc2 -o run --output-format csv -- python bench.py --config C2 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
         evab) for E in 1 2 4 1 2 4; do VTK_EV_EVERY=$E step evab_c2_$E 300 python bench.py --config C2 --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; python tools/bench_brief.py gpurun_out/evab_c2_$E.log; VTK_EV_EVERY=$E step evab_solo_$E 300 python bench.py --config C2 --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 5 --comm-solo || exit $?; python tools/bench_brief.py gpurun_out/evab_solo_$E.log; done ;;
+        profall) for C in C3 C4; do c=$(echo $C | tr C c); A="--config $C --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5";
+                 step prof_$c 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline || exit $?;
+                 step pmcf_$c 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_$c -o run --output-format csv -- python bench.py $A || exit $?;
+                 step pmcw_$c 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_$c -o run --output-format csv -- python bench.py $A || exit $?;
+                 step pmcsq_$c 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES -d gpurun_out/pmcsq_$c -o run --output-format csv -- python bench.py $A || exit $?; done ;;
         large) step large 600 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

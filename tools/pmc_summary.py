@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--write", default="pmc_write")
     ap.add_argument("--cmd", default="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5")
     ap.add_argument("--config", default="C3", help="bench config the profiled command ran (bench.py matches it)")
+    ap.add_argument("--sq", default=None, help="dir of a --pmc SQ_* pass: per-kernel mean counters -> <tag>pmc_sq.json")
     ap.add_argument("--patch-bench", default=None,
                     help="bench JSON (one line) of the same call whose roofline traffic fields are refreshed "
                          "from this summary (the bench ran before the PMC passes)")
@@ -114,6 +115,23 @@ def main():
         f_kib, w_kib = statistics.mean(fk), statistics.mean(wk) if wk else 0.0
         out["kernels"][cls] = {"dispatches": len(fk), "fetch_kib": f_kib, "write_kib": w_kib,
                                "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024}
+    if a.sq:
+        rows = collections.defaultdict(lambda: collections.defaultdict(list))
+        with open(os.path.join(src, a.sq, "run_counter_collection.csv")) as f:
+            for r in csv.DictReader(f):
+                rows[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        sq = {"_how": f"rocprofv3 --pmc SQ_* of '{a.cmd}'; mean per dispatch; wait fraction = SQ_WAIT_ANY / SQ_WAVE_CYCLES",
+              "config": a.config, "kernels_sha16": ksha, "kernels": {}}
+        for k, cs in rows.items():
+            if not any(re.match(p if p.startswith("void") else re.escape(p), k + "(") for p in CLASSES.values()):
+                continue
+            m = {c: statistics.mean(v) for c, v in cs.items()}
+            if m.get("SQ_WAVE_CYCLES"):
+                m["wait_frac"] = m.get("SQ_WAIT_ANY", 0.0) / m["SQ_WAVE_CYCLES"]
+            sq["kernels"][k] = m
+        with open(os.path.join(prof, f"{tag}pmc_sq.json"), "w") as f:
+            json.dump(sq, f, indent=1)
+        print("wrote", os.path.join(prof, f"{tag}pmc_sq.json"))
     dst = os.path.join(prof, f"{tag}pmc_traffic.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)

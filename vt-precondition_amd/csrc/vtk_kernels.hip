@@ -1151,6 +1151,12 @@ template <typename VT, bool HALO, int EPI, int MAXBS>
 static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, bool sell, dim3 g, hipStream_t s) {
     const dim3 blk(NT);
     if (tri) {
+        // 9-wide uniform rows (C4): the compile-time-width path (the cycle-start residual
+        // kernel, 1440 us with the runtime loop)
+        if (EPI != EPI_PREC_DC && VTK_SELL_WU && sell && bs == 8 && a.sell_uw == 9) {
+            hipLaunchKernelGGL((k_sell<VT, HALO, EPI, 8, true, 0, 9>), g, blk, 0, s, a);
+            return hipGetLastError();
+        }
         switch (bs) {
             case 2: VTK_SPMV_LAUNCH(EPI, 2, true); break;
             case 4: VTK_SPMV_LAUNCH(EPI, 4, true); break;
