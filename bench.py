@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--seg", type=int, default=25, help="line-Jacobi segment length (x-points)")
     ap.add_argument("--comm-solo", action="store_true",
                     help="one GPU through the distributed code paths (one-rank RCCL communicator)")
+    ap.add_argument("--slab", type=int, default=1,
+                    help="run one rank's slab of the config at this GPU count (Nx / SLAB x-columns; "
+                         "with --comm-solo: the per-rank distributed step on one GPU)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="rccl (production) or host-staged hooks over gloo (testing: ranks may share a GPU)")
     ap.add_argument("--check-launch", action="store_true",
@@ -244,6 +247,13 @@ def main():
     dev = torch.device("cuda", device)
 
     dim, shape, fp32 = CONFIGS[args.config]
+    if args.slab > 1:
+        # one rank's share of the config at --slab GPUs: the x-direction cut by that many (the
+        # same periodic operator on Nx / P columns), run through the distributed code paths
+        # (--comm-solo): the per-rank step time of a P-GPU run without its xGMI transfers
+        if world != 1 or shape[0] % args.slab:
+            raise SystemExit("--slab needs one rank and Nx divisible by it")
+        shape = (shape[0] // args.slab,) + tuple(shape[1:])
     params = vk.vlasov_params(dim, shape, fp32=fp32)
     n_glob = int(np.prod(shape))
     align = shape[-1] if dim == 2 else shape[-1] * shape[-2] * shape[-3]   # x-slab boundaries
@@ -444,7 +454,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64" if not fp32 else "f32-values/f64",
         "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
-        "config": {"workload": f"{args.config}: GMRES({args.restart}, {args.orth})+{mdesc} to rtol={args.rtol}, "
+        "config": {"workload": f"{args.config}{'/' + str(args.slab) + ' slab' if args.slab > 1 else ''}: "
+                               f"GMRES({args.restart}, {args.orth})+{mdesc} to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
                    "prec": args.prec, "bs": args.bs if args.prec == "bj" else None,

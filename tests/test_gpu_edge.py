@@ -61,3 +61,26 @@ def test_zero_rhs_and_empty(gpu, vk_lib):
     assert (E @ np.zeros(0)).shape == (0,)
     with pytest.raises(ValueError):
         vk.gmres(E, np.zeros(0))
+
+
+def test_device_csr_input(gpu, vk_lib):
+    """CSR arrays already in HBM (VTK_PTR_DEVICE): the same operator as the host path, and a
+    column index out of [0, n) is rejected by the device range check instead of
+    reaching the SpMV gathers."""
+    import torch
+    vk = vk_lib
+    n = 300
+    ip, ix, d = tridiag(n)
+    dev = torch.device("cuda", 0)
+    A = vk.csr_matrix((torch.from_numpy(d).to(dev), torch.from_numpy(ix).to(dev), torch.from_numpy(ip).to(dev)),
+                      shape=(n, n), ctx=gpu)
+    x = twin.rhs(n, seed=0xC0FFEE)
+    assert np.array_equal(A @ x, coracle.spmv(ip, ix, d, x))
+    for bad in (n, -1, 1 << 30):
+        ixb = ix.copy()
+        ixb[n // 2] = bad
+        with pytest.raises(vk._abi.VtkError, match="column index out of range"):
+            vk.csr_matrix((torch.from_numpy(d).to(dev), torch.from_numpy(ixb).to(dev), torch.from_numpy(ip).to(dev)),
+                          shape=(n, n), ctx=gpu)
+        with pytest.raises(vk._abi.VtkError, match="column index out of range"):
+            vk.csr_matrix((d, ixb, ip), shape=(n, n), ctx=gpu)

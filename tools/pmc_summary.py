@@ -34,7 +34,8 @@ CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv
     "spmv_csr": r"void vtk::k_spmv<(double|float), false, 0, 1",
     "spmv_bj_dc_csr": r"void vtk::k_spmv<(double|float), false, 4, 8",
     "dc_dots": "void vtk::k_dc_dots_rows<",
-    "line_apply": "void vtk::k_line_apply<",
+    "line_dc": r"void vtk::k_line_apply<\d+, (true|false), true>",
+    "line_apply": r"void vtk::k_line_apply<\d+, (true|false)(, false)?>",
     "dc_update": "void vtk::k_dc_update<",
     "dc_scalar": "vtk::k_dc_scalar(",
     "mgs": "vtk::k_mgs(",

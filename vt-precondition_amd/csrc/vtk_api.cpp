@@ -10,6 +10,7 @@
 // without a per-step round trip and throttles itself with events LOOKAHEAD columns behind.
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -619,6 +620,9 @@ void destroy_csr(vtk_csr *A) {
 #ifndef VTK_DC_FUSED
 #define VTK_DC_FUSED 1   // DCGS2 dots inside the SpMV + BJ kernel (0: SpMV + BJ, then k_dc_dots)
 #endif
+#ifndef VTK_LINE_DC
+#define VTK_LINE_DC 1    // line path: DCGS2 dots inside the line-apply kernel (0: k_dc_dots after it)
+#endif
 
 struct Solver {
     vtk_csr *A;
@@ -683,6 +687,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // SpMV + BJ and the step's dots in one pass for BJ-fused tiles with bs <= 8 (larger blocks
     // would spill the fused kernel's registers)
     const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8;
+    // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
+    const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
+                         s.M->line.seg <= 32 && s.G <= GMAX;
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = matrix_bytes(s.A);
     const double b_inv = bj_row_bytes(s.M) * n;
@@ -752,6 +759,15 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             const SpmvIn in = spmv_in(s.A, ft, pj);
             HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             cnt = spmv_grid(in);
+        } else if (line_dc) {
+            // line path: SpMV, then the line sweeps with the step's dots fused behind them
+            TRY(halo_exchange(s.A, pj));
+            { Prof pf(c, "spmv", j, b_csr + 2 * n8);
+              HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
+                                    nullptr, stop, j, c->stream)); }
+            { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
+              HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream)); }
+            cnt = s.G;
         } else {
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
@@ -1179,6 +1195,17 @@ int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t
     if (nnz) {
         HIPCHK(c, hipMemcpy(A->d_indices, indices, nnz * sizeof(int32_t), kd));
         HIPCHK(c, hipMemcpy(A->d_data, data, nnz * vb, kd));
+    }
+    if (kind == VTK_PTR_DEVICE && nnz) {   // device input: the same range check on the device
+        DBuf mmb;
+        TRY(dalloc(c, mmb, 2 * sizeof(int)));
+        int mm[2] = {INT_MAX, INT_MIN};
+        HIPCHK(c, hipMemcpy(mmb.p, mm, sizeof(mm), hipMemcpyHostToDevice));
+        HIPCHK(c, launch_index_range(A->d_indices, nnz, mmb.as<int>(), c->stream));
+        HIPCHK(c, hipMemcpyAsync(mm, mmb.p, sizeof(mm), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (mm[0] < 0 || (int64_t)mm[1] >= n_global)
+            return fail(c, VTK_ERR_ARG, "vtk_csr_create: column index out of range");
     }
     TRY(finish_csr(A));
     *out = A;

@@ -216,6 +216,9 @@ struct BjOp {
     const LineOp *line = nullptr;   // line Jacobi instead (inv/tri unused)
 };
 
+// mm[0] = min, mm[1] = max of idx[0..n) (mm preset to INT_MAX, INT_MIN)
+hipError_t launch_index_range(const int32_t *idx, int64_t n, int *mm, hipStream_t s);
+
 // workgroups (= partials) of a launch on this input
 inline int spmv_grid(const SpmvIn &in) { return (in.sell && in.groups) ? in.groups->grid : in.tiles->grid; }
 
@@ -251,6 +254,10 @@ hipError_t launch_sell_pack(const int64_t *off, int64_t nch, int64_t *pkoff, int
 // z = M^-1 r with part0 = sum z^2, part1 = sum v0*z (optional) over `grid` workgroups
 hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
                              const LineOp &L, unsigned long long *bad_row, unsigned long long *ext, hipStream_t s);
+// z = M_line^-1 r fused with DCGS2 step j's dots (p = the SpMV input, partials in the
+// launch_dc_dots layout); hipErrorInvalidValue when the segments are too long (> 32)
+hipError_t launch_line_dc(const LineOp &L, const double *r, double *w, const double *V, int64_t ld, int j,
+                          const double *p, double *part, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_line_apply(const LineOp &L, const double *r, double *z, const double *v0, double *part0,
                              double *part1, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,

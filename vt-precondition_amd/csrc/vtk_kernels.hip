@@ -14,6 +14,7 @@
 
 #include <float.h>
 
+#include <climits>
 #include <cstdlib>
 
 #include "vtk_internal.hpp"
@@ -1572,16 +1573,31 @@ __global__ __launch_bounds__(NT) void k_line_setup(const int32_t *__restrict__ i
 // (L.ac) - 16 B/row read instead of 32; the same IEEE operations as the stored factors.
 // LMAX == 0 (segments longer than 32): d goes through z.  r and z may alias (each row is read
 // before it is written, by its lane).
-template <int LMAX, bool COMPACT>
+// DCD (DCGS2 step j, line path): the step's dots fused behind the sweep -- w = z stays in the
+// lane's registers, p and the basis rows of the lane's segment rows are read once here:
+// s = V_j^T p, z = V_j^T w, ||p||^2, p.w, ||w||^2 as per-workgroup partials in launch_dc_dots'
+// layout (dc.part[q * GMAX + block]); no separate dots kernel re-reads w.
+struct LineDc {
+    const double *V;
+    int64_t ld;
+    int j;
+    const double *p;
+    double *part;
+};
+template <int LMAX, bool COMPACT, bool DCD = false>
 __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, double *z,
                                                    const double *__restrict__ v0, double *part0,
-                                                   double *part1, const int *stop_col, int col) {
+                                                   double *part1, const int *stop_col, int col,
+                                                   LineDc dc = LineDc{}) {
     __shared__ double red[NT / 64];
+    constexpr int NQW = 2 * DC_MAXJ + 3;
+    __shared__ double stage[DCD ? (NT / 64) * NQW : 1];
     if (stopped(stop_col, col)) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t nitems = L.nseg * L.jb, S = L.stride, r0 = L.row0, r_end = L.row0 + L.n;
     const double *l = L.f, *m = L.f + L.n, *g = L.f + 2 * L.n;
     double acc0 = 0.0, acc1 = 0.0;
+    [[maybe_unused]] double dsl = 0.0, dzl = 0.0, daa = 0.0, dab = 0.0, dag = 0.0;   // DCD
     for (int64_t t = (int64_t)blockIdx.x * (NT / 64) + wv; t < nitems; t += (int64_t)gridDim.x * (NT / 64)) {
         const LineLane q = line_lane(L, t, lane);
         const int64_t len = q.i_end - q.i_beg;
@@ -1634,8 +1650,43 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
                     const int k = (int)(k0l + (int64_t)u * S);
                     st_nt<4>(z + k, zv);
                     zn = zv;
-                    acc0 += zv * zv;
-                    if (v0) acc1 += v0[k] * zv;
+                    if constexpr (!DCD) {
+                        acc0 += zv * zv;
+                        if (v0) acc1 += v0[k] * zv;
+                    }
+                }
+                if constexpr (DCD) e[u] = ((okm >> u) & 1u) ? zv : 0.0;   // w, kept for the dots
+            }
+            if constexpr (DCD) {
+                // p on the lane's rows (gg is free after the sweep), then the basis vector by
+                // vector: all of the lane's rows of V_k in flight at once, summed in the lane and
+                // across the wave by the butterfly; lane k keeps the running sums of vector k
+#pragma unroll
+                for (int u = 0; u < LMAX; ++u) {
+                    const int k = (int)(k0l + (int64_t)u * S);
+                    gg[u] = ((okm >> u) & 1u) ? ld_nt<4>(dc.p + k) : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < LMAX; ++u) {
+                    daa += gg[u] * gg[u];
+                    dab += gg[u] * e[u];
+                    dag += e[u] * e[u];
+                }
+                for (int kk = 0; kk < dc.j; ++kk) {
+                    const double *vk = dc.V + (size_t)kk * dc.ld;
+                    double sl = 0.0, zl = 0.0;
+#pragma unroll
+                    for (int u = 0; u < LMAX; ++u) {
+                        const int k = (int)(k0l + (int64_t)u * S);
+                        const double v = ((okm >> u) & 1u) ? __builtin_nontemporal_load(vk + k) : 0.0;
+                        sl += v * gg[u];
+                        zl += v * e[u];
+                    }
+                    const double ts = wave_allsum(sl), tz = wave_allsum(zl);
+                    if (lane == kk) {
+                        dsl += ts;
+                        dzl += tz;
+                    }
                 }
             }
         } else {
@@ -1661,6 +1712,31 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
             }
         }
     }
+    if constexpr (DCD) {
+        // per-workgroup partials: the 4 waves' records summed in wave order
+        double *rec = stage + wv * NQW;
+        if (lane < dc.j) {
+            rec[lane] = dsl;
+            rec[DC_MAXJ + lane] = dzl;
+        }
+        const double t0 = wave_sum(daa), t1 = wave_sum(dab), t2 = wave_sum(dag);
+        if (lane == 0) {
+            rec[2 * DC_MAXJ] = t0;
+            rec[2 * DC_MAXJ + 1] = t1;
+            rec[2 * DC_MAXJ + 2] = t2;
+        }
+        __syncthreads();
+        for (int qq = threadIdx.x; qq < DC_NQ; qq += NT) {
+            const bool used = qq < dc.j || (qq >= DC_MAXJ && qq < DC_MAXJ + dc.j) || qq >= 2 * DC_MAXJ;
+            if (used) {
+                double t = 0.0;
+#pragma unroll
+                for (int w2 = 0; w2 < NT / 64; ++w2) t += stage[w2 * NQW + qq];
+                dc.part[(size_t)qq * GMAX + blockIdx.x] = t;
+            }
+        }
+        return;
+    }
     if (part0) {
         const double t0 = block_sum(acc0, red);
         if (threadIdx.x == 0) part0[blockIdx.x] = t0;
@@ -1678,6 +1754,26 @@ hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, cons
     const dim3 g((unsigned)((threads + NT - 1) / NT));
     if (fp32) hipLaunchKernelGGL(k_line_setup<float>, g, dim3(NT), 0, s, indptr, indices, (const float *)data, L, bad_row, ext);
     else hipLaunchKernelGGL(k_line_setup<double>, g, dim3(NT), 0, s, indptr, indices, (const double *)data, L, bad_row, ext);
+    return hipGetLastError();
+}
+
+// line apply + DCGS2 dots of step j (segments <= 32; else hipErrorInvalidValue: the caller
+// runs the unfused dots)
+hipError_t launch_line_dc(const LineOp &L, const double *r, double *w, const double *V, int64_t ld, int j,
+                          const double *p, double *part, int grid, const int *stop_col, int col, hipStream_t s) {
+    if (j > DC_MAXJ || grid > GMAX || L.seg > 32 || L.seg <= 0) return hipErrorInvalidValue;
+    const dim3 g(grid), b(NT);
+    const LineDc dc{V, ld, j, p, part};
+#define VTK_LINE_DC_LAUNCH(LM)                                                                               \
+    do {                                                                                                     \
+        if (L.compact) hipLaunchKernelGGL((k_line_apply<LM, true, true>), g, b, 0, s, L, r, w, nullptr, nullptr, nullptr, stop_col, col, dc); \
+        else hipLaunchKernelGGL((k_line_apply<LM, false, true>), g, b, 0, s, L, r, w, nullptr, nullptr, nullptr, stop_col, col, dc);        \
+    } while (0)
+    if (L.seg <= 8) VTK_LINE_DC_LAUNCH(8);
+    else if (L.seg <= 16) VTK_LINE_DC_LAUNCH(16);
+    else if (L.seg <= 25) VTK_LINE_DC_LAUNCH(25);
+    else VTK_LINE_DC_LAUNCH(32);
+#undef VTK_LINE_DC_LAUNCH
     return hipGetLastError();
 }
 
@@ -2142,6 +2238,32 @@ hipError_t launch_gather(const double *x, const int32_t *idx, int64_t cnt, doubl
 // ------------------------------------------------------------------------------------------
 // device-side operator assembly: counts -> exclusive scan -> fill
 // ------------------------------------------------------------------------------------------
+// min / max of device column indices (vtk_csr_create with device arrays validates them before
+// any SpMV gathers through them); integer atomics: exact in any order
+__global__ __launch_bounds__(NT) void k_index_range(const int32_t *__restrict__ idx, int64_t n, int *mm) {
+    int lo = INT_MAX, hi = INT_MIN;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+        const int v = idx[i];
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int ol = __shfl_xor(lo, off, 64), oh = __shfl_xor(hi, off, 64);
+        lo = ol < lo ? ol : lo;
+        hi = oh > hi ? oh : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(mm, lo);
+        atomicMax(mm + 1, hi);
+    }
+}
+
+hipError_t launch_index_range(const int32_t *idx, int64_t n, int *mm, hipStream_t s) {
+    hipLaunchKernelGGL(k_index_range, dim3(1024), dim3(NT), 0, s, idx, n, mm);
+    return hipGetLastError();
+}
+
 __global__ void k_vlasov_counts(vtk_vlasov_params p, int64_t r0, int64_t nrows, int32_t *counts) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * blockDim.x)
         counts[i] = vlasov_row_count(p, r0 + i);

@@ -246,6 +246,10 @@ class CsrOperator:
             pass
 
 
+def _is_device(a) -> bool:
+    return getattr(a, "is_cuda", False) is True
+
+
 def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
     """Build a device CSR operator from ``(data, indices, indptr)`` or a SciPy sparse matrix.
 
@@ -261,6 +265,23 @@ def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> 
         data, indices, indptr = arg
     if shape is None or shape[0] != shape[1]:
         raise ValueError("a square shape is required")
+    if _is_device(data) or _is_device(indices) or _is_device(indptr):
+        # CSR already in HBM (torch tensors on the context's device): no host round trip; the
+        # library validates indptr (host copy) and the column range (device reduction)
+        import torch
+        if not (_is_device(data) and _is_device(indices) and _is_device(indptr)):
+            raise TypeError("csr_matrix: data, indices and indptr must all be device tensors or all host arrays")
+        fp32 = data.dtype == torch.float32
+        data = data.contiguous().to(torch.float32 if fp32 else torch.float64)
+        indices = indices.contiguous().to(torch.int32)
+        indptr = indptr.contiguous().to(torch.int32)
+        offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
+        h = C.c_void_p()
+        check(lib().vtk_csr_create(ctx.handle, int(shape[0]), None if offs is None else _np_ptr(offs),
+                                   int(indices.numel()), C.c_void_p(indptr.data_ptr()),
+                                   C.c_void_p(indices.data_ptr()), C.c_void_p(data.data_ptr()),
+                                   int(fp32), _abi.PTR_DEVICE, C.byref(h)), ctx.handle)
+        return CsrOperator(h, ctx, fp32)
     data = np.asarray(data)
     fp32 = data.dtype == np.float32
     data = np.ascontiguousarray(data, dtype=np.float32 if fp32 else np.float64)
