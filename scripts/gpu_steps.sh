@@ -64,6 +64,12 @@ for s in "$@"; do
                  step pmcf_$c 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_$c -o run --output-format csv -- python bench.py $A || exit $?;
                  step pmcw_$c 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_$c -o run --output-format csv -- python bench.py $A || exit $?;
                  step pmcsq_$c 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES -d gpurun_out/pmcsq_$c -o run --output-format csv -- python bench.py $A || exit $?; done ;;
+        slabs) step slab_c3_8 300 python bench.py --config C3 --slab 8 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
+               step slab_c3_4 300 python bench.py --config C3 --slab 4 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
+               step slab_c3_2 300 python bench.py --config C3 --slab 2 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
+               step slab_c3_1 300 python bench.py --config C3 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
+               step slab_c4_8 300 python bench.py --config C4 --slab 8 --comm-solo --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+        benchc2full) step benchc2full 600 python bench.py --config C2 ;;
         large) step large 600 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -79,8 +79,8 @@ def test_device_csr_input(gpu, vk_lib):
     for bad in (n, -1, 1 << 30):
         ixb = ix.copy()
         ixb[n // 2] = bad
-        with pytest.raises(vk._abi.VtkError, match="column index out of range"):
+        with pytest.raises(ValueError, match="column index out of range"):
             vk.csr_matrix((torch.from_numpy(d).to(dev), torch.from_numpy(ixb).to(dev), torch.from_numpy(ip).to(dev)),
                           shape=(n, n), ctx=gpu)
-        with pytest.raises(vk._abi.VtkError, match="column index out of range"):
+        with pytest.raises(ValueError, match="column index out of range"):
             vk.csr_matrix((d, ixb, ip), shape=(n, n), ctx=gpu)
