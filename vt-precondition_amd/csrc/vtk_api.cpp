@@ -634,6 +634,7 @@ struct Solver {
     double *part[4];
     double *Hraw = nullptr, *dcpart = nullptr;   // DCGS2
     DcCoef *cf = nullptr;
+    double *x = nullptr;                         // the solution (the DCGS2 update pass may update it)
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
@@ -774,7 +775,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         }
         TRY(reduce_step(j, s.w, j, cnt));
         { Prof pf(c, "dc_update", j, n8 * (j + 4));
-          HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, stop, fused ? 0 : 1, c->stream)); }
+          HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
+                                     c->stream)); }
         // throttle: an event every EV_EVERY steps (each record costs the stream a few us); the
         // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
         // has passed there.  Column cc stops in step cc (early commit) or cc+1: act only once
@@ -809,6 +811,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const int m = restart;
     Solver s{A, M, c, n, round_up(std::max<int64_t>(n, 1), 64), m, grid_for(c, vector_grid(n)), nullptr, nullptr,
              nullptr, nullptr, nullptr, nullptr, nullptr, {c->d_part, c->d_part + GMAX, c->d_part + 2 * GMAX, c->d_part + 3 * GMAX}};
+    s.x = x;
     // workspace: V[(m+1) x ld] | w | tmp | r | H[m x (m+1)] | S[m+1] | giv[2m]  (doubles)
     const bool dc = c->orth == VTK_ORTH_DCGS2 || (c->orth == VTK_ORTH_AUTO && m <= DC_MAXJ);
     if (dc && m > DC_MAXJ) return fail(c, VTK_ERR_ARG, "DCGS2 supports restart <= 32 (use VTK_ORTH_MGS)");
@@ -841,6 +844,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     GmresState *ds = c->d_state, *hs = c->h_state;
     std::memset(hs, 0, sizeof(GmresState));
     hs->stop_col = BIG_COL;
+    hs->xup_tag = -1;
     HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(GmresState), hipMemcpyHostToDevice, c->stream));
     int rc;
     const double n8 = 8.0 * n;
@@ -993,7 +997,18 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         HIPCHK(c, hipStreamSynchronize(c->stream));
         const int last = hs->stop_col < m ? hs->stop_col : m - 1;
         if (c->prof_on) {
-            if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].bytes = n8 * (last + 1) + 2 * n8;
+            const double xb = n8 * (last + 1) + 2 * n8;   // V[0..last] (or V_last and p_last), x in/out
+            if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].bytes = xb;
+            if (hs->xup_tag >= 0) {
+                // the x update ran in update pass xup_tag: account it as the "xupdate" class and
+                // drop the host-enqueued k_xupdate (it returned at entry)
+                const int cu = prof_class(c, "dc_update"), cx = prof_class(c, "xupdate");
+                for (size_t i = 0; i < xup_idx && i < c->prof_pending.size(); ++i) {
+                    auto &p = c->prof_pending[i];
+                    if (p.cls == cu && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
+                }
+                if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].col = BIG_COL;
+            }
             prof_flush(c, last);
         }
         for (int j = 0; j <= last; ++j) st.bytes_moved += bytes_spmv + bytes_pc + 8.0 * n * (2 * j + 8);

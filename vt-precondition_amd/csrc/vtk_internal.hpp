@@ -29,6 +29,9 @@ struct GmresState {
     int stop_col;         // column at which the cycle stopped (BIG_COL while running)
     int breakdown;        // h1 <= eps*h0 at stop_col
     long long inner;      // inner iterations, cumulative
+    int xup_tag;          // DCGS2: the update pass (step tag) that does the cycle's x update
+                          // (-1: none, the host-enqueued k_xupdate does it)
+    int pad_;
 };
 
 // DCGS2 (delayed classical Gram-Schmidt with re-orthogonalisation, one reduction per Arnoldi
@@ -279,6 +282,7 @@ hipError_t launch_tail(Red h0, Red w2, const double *w, double *vnext, int64_t n
 hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresState *st,
                          int grid, hipStream_t s);
 // y = triangular solve (H, S) at stop column; x += y @ V
+// (returns at entry when a DCGS2 update pass already did it: st->xup_tag >= 0)
 hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld,
                           double *x, int64_t n, int m, const GmresState *st, int grid,
                           hipStream_t s);
@@ -317,8 +321,12 @@ hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, do
 hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int j, int m,
                             int closing, double *Hraw, double *H, double *S, double *giv,
                             DcCoef *cf, GmresState *st, int *stop_map, hipStream_t s);
+// update pass of step j; when the step's scalar kernel stopped the cycle (st->xup_tag == j) it
+// does the cycle's x update instead: x += V[0..c] y, y = H^-1 S at c = stop_col (j-1 or j; for
+// c = j the v_j of the pass is formed in registers), reading the basis once
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
-                            const DcCoef *cf, int grid, const int *stop_col, int nt_pw, hipStream_t s);
+                            const DcCoef *cf, int grid, const GmresState *st, double *x,
+                            const double *H, const double *S, int m, int nt_pw, hipStream_t s);
 
 int vector_grid(int64_t n);
 

@@ -2122,6 +2122,7 @@ __global__ __launch_bounds__(NT) void k_scale0(Red p, double *__restrict__ v0, i
         S[0] = t;
         st->stop_col = BIG_COL;
         st->breakdown = 0;
+        st->xup_tag = -1;
     }
 }
 
@@ -2135,25 +2136,30 @@ hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresSt
 // x += y @ V[0..col] with y from the (m+1) x m Hessenberg least squares
 // (iterative.py:799-814).  Workgroup-redundant triangular solve on lane 0, into LDS.
 // ------------------------------------------------------------------------------------------
+// y = H^-1 S over columns 0..col (lane 0 of a workgroup, into LDS ys; iterative.py:799-812)
+__device__ inline void hess_solve(const double *__restrict__ H, const double *__restrict__ S, int m, int col,
+                                  double *ys) {
+    const int M1 = m + 1;
+    for (int k = 0; k <= col; ++k) ys[k] = S[k];
+    if (H[(size_t)col * M1 + col] == 0.0) ys[col] = 0.0;
+    for (int k = col; k > 0; --k) {
+        if (ys[k] != 0.0) {
+            ys[k] = ys[k] / H[(size_t)k * M1 + k];
+            const double t = ys[k];
+            for (int i = 0; i < k; ++i) ys[i] = ys[i] - t * H[(size_t)k * M1 + i];
+        }
+    }
+    if (ys[0] != 0.0) ys[0] = ys[0] / H[0];
+}
+
 __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, const double *__restrict__ S,
                                                 const double *__restrict__ V, int64_t ld,
                                                 double *__restrict__ x, int64_t n, int m,
                                                 const GmresState *st) {
     extern __shared__ __attribute__((aligned(16))) double ys[];
+    if (st->xup_tag >= 0) return;   // a DCGS2 update pass did it
     const int col = st->stop_col < m ? st->stop_col : m - 1;
-    if (threadIdx.x == 0) {
-        const int M1 = m + 1;
-        for (int k = 0; k <= col; ++k) ys[k] = S[k];
-        if (H[(size_t)col * M1 + col] == 0.0) ys[col] = 0.0;
-        for (int k = col; k > 0; --k) {
-            if (ys[k] != 0.0) {
-                ys[k] = ys[k] / H[(size_t)k * M1 + k];
-                const double t = ys[k];
-                for (int i = 0; i < k; ++i) ys[i] = ys[i] - t * H[(size_t)k * M1 + i];
-            }
-        }
-        if (ys[0] != 0.0) ys[0] = ys[0] / H[0];
-    }
+    if (threadIdx.x == 0) hess_solve(H, S, m, col, ys);
     __syncthreads();
     const int64_t stride = 2 * (int64_t)gridDim.x * NT;
     for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
@@ -2632,6 +2638,7 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
         if (presid <= ptol || brk) {
             st->breakdown = brk ? 1 : 0;
             st->stop_col = c;
+            if (!closing) st->xup_tag = j;   // this step's update pass does the x update
             if (stop_map) __hip_atomic_store(stop_map, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return true;
         }
@@ -2720,6 +2727,7 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
     cf->committed[j] = 1;
     if (!rotate_commit(j, false) && last) {
         st->stop_col = j;   // cycle complete: later kernels of this cycle are no-ops
+        st->xup_tag = j;
         if (stop_map) __hip_atomic_store(stop_map, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -2736,15 +2744,83 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 #ifndef VTK_UPD_NT
 #define VTK_UPD_NT 2   // non-temporal stores in the update pass: 1 v_j, 2 v_j and p_{j+1} (A/B: 2 = +2.6 % it/s)
 #endif
+#ifndef VTK_XUP_FUSED
+#define VTK_XUP_FUSED 1   // the cycle's x update inside the stopping step's update pass (one basis read less per cycle)
+#endif
+// The cycle's x update in the update pass of the step whose scalar kernel stopped it (xup_tag):
+// c = stop_col is j-1 (column j-1 finalised in step j: V[0..j-1] all stored) or j (column j
+// committed early: v_j = (p_j - V_j s) / r formed here exactly as the normal pass would store
+// it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
+__device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
+                                        const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
+                                        const double *__restrict__ S, int m) {
+    __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ];
+    __shared__ double rinv_s;
+    if (threadIdx.x == 0) {
+        hess_solve(H, S, m, c, ys);
+        rinv_s = cf->rinv;
+    }
+    if (c == j)
+        for (int k = threadIdx.x; k < j; k += NT) cs[k] = cf->s[k];
+    __syncthreads();
+    const double rinv = rinv_s;
+    const double *pj = V + (size_t)j * ld;
+    const int kv = c == j ? j : c + 1;   // stored basis vectors in the sum
+    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            double ax = 0.0, ay = 0.0;
+            double2 a = make_double2(0.0, 0.0);
+            if (c == j) {
+                const d2v pp = ldnt2(pj + i);
+                a = make_double2(pp.x, pp.y);
+            }
+            for (int k = 0; k < kv; ++k) {
+                const d2v v = ldnt2(V + (size_t)k * ld + i);
+                ax += ys[k] * v.x;
+                ay += ys[k] * v.y;
+                if (c == j) {
+                    const double sk = cs[k];
+                    a.x = a.x - sk * v.x;
+                    a.y = a.y - sk * v.y;
+                }
+            }
+            if (c == j) {
+                const double vx = j >= 1 ? a.x * rinv : a.x, vy = j >= 1 ? a.y * rinv : a.y;
+                ax += ys[j] * vx;
+                ay += ys[j] * vy;
+            }
+            double2 xv = *reinterpret_cast<const double2 *>(x + i);
+            xv.x = xv.x + ax;
+            xv.y = xv.y + ay;
+            st_nt2<1>(x + i, xv.x, xv.y);
+        } else {
+            double ax = 0.0, a = c == j ? pj[i] : 0.0;
+            for (int k = 0; k < kv; ++k) {
+                const double v = V[(size_t)k * ld + i];
+                ax += ys[k] * v;
+                if (c == j) a = a - cs[k] * v;
+            }
+            if (c == j) ax += ys[j] * (j >= 1 ? a * rinv : a);
+            x[i] = x[i] + ax;
+        }
+    }
+}
+
 // NTPW: p_j and w loaded non-temporal (A/B: +2 % on the unfused (line) path, -1 % after the
 // fused BJ step, whose w the update re-reads warm)
 template <bool NTPW>
 __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_t ld, int j,
                                                   const double *__restrict__ w, int64_t n,
-                                                  const DcCoef *cf, const int *stop_col) {
+                                                  const DcCoef *cf, const GmresState *st, double *x,
+                                                  const double *H, const double *S, int m) {
     __shared__ double cs[DC_MAXJ], ce[DC_MAXJ + 1];
     __shared__ double rinv_s, q_s;
-    if (stopped(stop_col, j)) return;
+    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&st->xup_tag) == j) {
+        dc_xupdate(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m);
+        return;
+    }
+    if (stopped(&st->stop_col, j)) return;
     for (int k = threadIdx.x; k <= j; k += NT) {
         if (k < j) cs[k] = cf->s[k];
         ce[k] = cf->e[k];
@@ -2805,12 +2881,13 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
 }
 
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n, const DcCoef *cf,
-                            int grid, const int *stop_col, int nt_pw, hipStream_t s) {
+                            int grid, const GmresState *st, double *x, const double *H, const double *S, int m,
+                            int nt_pw, hipStream_t s) {
 #ifdef VTK_UPD_NTPW_FORCE
     nt_pw = VTK_UPD_NTPW_FORCE;
 #endif
-    if (nt_pw) hipLaunchKernelGGL(k_dc_update<true>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, stop_col);
-    else hipLaunchKernelGGL(k_dc_update<false>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, stop_col);
+    if (nt_pw) hipLaunchKernelGGL(k_dc_update<true>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+    else hipLaunchKernelGGL(k_dc_update<false>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
     return hipGetLastError();
 }
 
