@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTK_ABI_VERSION 1
+#define VTK_ABI_VERSION 2
 
 typedef struct vtk_ctx vtk_ctx;
 typedef struct vtk_csr vtk_csr;
@@ -110,6 +110,7 @@ typedef struct {
     double bytes_moved;    /* algorithmic HBM bytes of the solve           */
     int breakdown;         /* 1 if the last cycle hit h1 <= eps*h0                        */
     int orth;              /* vtk_orth used                                               */
+    int band;              /* 1: the line-band DCGS2 step ran (vtk_csr_set_line_band)      */
 } vtk_stats;
 
 /* ---- library ------------------------------------------------------------------------ */
@@ -186,6 +187,15 @@ void vtk_csr_destroy(vtk_csr *A);
 int vtk_csr_set_layout(vtk_csr *A, int layout);
 int vtk_csr_get_layout(vtk_csr *A, int *layout_in_use);
 int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out);
+/* Line-band structure: rows form x-lines of `line_len` consecutive rows and
+ * every column lies in the lines x-1, x, x+1 (mod n / line_len) of its row's line x -- the 2D
+ * Vlasov operators with line_len = Nv (set automatically by vtk_csr_create_vlasov on one rank).
+ * Checked on the device (VTK_ERR_ARG when the structure does not hold; line_len 0 clears it).
+ * With it, vtk_gmres runs each DCGS2 update pass together with the next step's SpMV + BJ +
+ * dots in one sweep (SELL layout, tridiagonal BJ(8), restart <= 20, one rank): the basis is
+ * read once per Arnoldi step instead of twice.  Same operator, same update arithmetic. */
+int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len);
+int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len);
 
 /* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged
  * internally over RCCL when world > 1).  Bit-identical to csr_matvec (serial row sums). */
@@ -234,6 +244,9 @@ int vtk_prec_kind_of(vtk_prec *M, int *kind);
 int vtk_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, double atol,
               int restart, int64_t maxiter, int ptr_kind, int *info, vtk_stats *stats);
 int vtk_gmres_set_orth(vtk_ctx *ctx, int orth);
+/* on (default) / off: the line-band DCGS2 step when the operator and preconditioner allow it
+ * (vtk_csr_set_line_band); off keeps the separate update pass and fused SpMV step */
+int vtk_gmres_set_band(vtk_ctx *ctx, int on);
 
 /* ---- kernel profile (measurement) ------------------------------------------
  * When enabled, every kernel the library launches is bracketed by HIP events on the

@@ -1,0 +1,143 @@
+"""Line-band DCGS2 step (vtk_kernels.hip k_band_step): the update pass of step j
+fused with step j+1's SpMV + tridiagonal BJ(8) + dots in one sweep over x-lines.
+
+The band step performs the same update arithmetic as k_dc_update and the same SpMV / BJ
+arithmetic as k_sell (v_j, p_{j+1} and w bit-identical for the same inputs); only the dot
+products are summed in another fixed order.  So the solve follows the DCGS2 bars of
+tests/test_gpu_parity.py against the band-off path, the C oracle (SciPy's sequence) and SciPy's
+own summaries: same info, inner iterations +-1, ||x - x_ref|| / ||x_ref|| <= 1e-9, plus a
+bit-identical repeat (deterministic reductions).  Full size (C2, C3): tests/test_gpu_large.py
+runs the default path, which is this one (asserted there via stats.band).
+"""
+import numpy as np
+import pytest
+
+from oracle import coracle, twin
+
+pytestmark = pytest.mark.gpu
+
+
+def _op(vk, gpu, name):
+    p = twin.CONFIGS[name]
+    return p, vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=gpu)
+
+
+def _solve(vk, gpu, A, M, b, band, **kw):
+    gpu.set_band(band)
+    try:
+        x, info = vk.gmres(A, b, rtol=kw.pop("rtol", 1e-8), M=M, **kw)
+    finally:
+        gpu.set_band(True)
+    return x, info, vk.last_stats()
+
+
+@pytest.mark.parametrize("name", ["S2", "C1"])
+def test_band_detected_on_2d_vlasov(vk_lib, gpu, name):
+    p, A = _op(vk_lib, gpu, name)
+    assert A.line_band == p.shape[1]
+    A.close()
+
+
+def test_band_not_set_on_4d_and_rejected_on_random(vk_lib, gpu):
+    p, A = _op(vk_lib, gpu, "S4")
+    assert A.line_band == 0
+    # the 4D operator's x-couplings are Ny*Nvx*Nvy rows away: not within lines of Nvy rows
+    with pytest.raises(ValueError):
+        A.set_line_band(p.shape[3])
+    A.close()
+    import scipy.sparse as sp
+    R = sp.random(640, 640, density=0.02, random_state=3, format="csr") + sp.identity(640, format="csr")
+    B = vk_lib.csr_matrix(R.tocsr(), ctx=gpu)
+    with pytest.raises(ValueError):
+        B.set_line_band(64)
+    B.set_line_band(0)
+    assert B.line_band == 0
+    B.close()
+
+
+def test_band_explicit_on_uploaded_csr(vk_lib, gpu):
+    """A SciPy CSR of the 2D operator uploaded as plain CSR: set_line_band enables the path."""
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = coracle.generate(p)
+    import scipy.sparse as sp
+    A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    assert A.line_band == 0
+    A.set_line_band(p.shape[1])
+    assert A.line_band == p.shape[1]
+    M = vk_lib.block_jacobi(A, 8)
+    b = coracle.rhs(p.n)
+    x, info, st = _solve(vk_lib, gpu, A, M, b, True)
+    assert st.band == 1 and info == 0
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    assert abs(st.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    M.close()
+    A.close()
+
+
+@pytest.mark.parametrize("restart", [2, 5, 20])
+@pytest.mark.parametrize("name", ["S2", "C1"])
+def test_band_vs_unfused_and_oracle(vk_lib, gpu, name, restart):
+    p, A = _op(vk_lib, gpu, name)
+    M = vk_lib.block_jacobi(A, 8)
+    assert M.mode == "tridiag"
+    ip, ix, d = A.download()
+    b = coracle.rhs(p.n)
+    xb, ib, sb = _solve(vk_lib, gpu, A, M, b, True, restart=restart, maxiter=400)
+    xu, iu, su = _solve(vk_lib, gpu, A, M, b, False, restart=restart, maxiter=400)
+    assert sb.band == 1 and su.band == 0
+    assert ib == iu == 0
+    assert abs(sb.inner_iters - su.inner_iters) <= 1
+    assert np.linalg.norm(xb - xu) / np.linalg.norm(xu) < 1e-9
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8, restart=restart, maxiter=400)
+    assert ref.info == 0 and abs(sb.inner_iters - ref.inner_iters) <= 1, (sb.inner_iters, ref.inner_iters)
+    assert np.linalg.norm(xb - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    # the true residual, recomputed on the host
+    assert np.linalg.norm(b - coracle.spmv(ip, ix, d, xb)) <= 1e-8 * np.linalg.norm(b) * 1.0001
+    M.close()
+    A.close()
+
+
+def test_band_nonzero_x0_and_repeat(vk_lib, gpu):
+    p, A = _op(vk_lib, gpu, "C1")
+    M = vk_lib.block_jacobi(A, 8)
+    ip, ix, d = A.download()
+    b = coracle.rhs(p.n)
+    x0 = twin.rhs(p.n, seed=0xB00) * 1e-3
+    x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, True, x0=x0.copy())
+    x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, True, x0=x0.copy())
+    assert s1.band == 1 and i1 == i2 == 0
+    assert np.array_equal(x1, x2), "band solve not bit-identical on repeat"
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), x0=x0.copy(), rtol=1e-8)
+    assert abs(s1.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(x1 - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    M.close()
+    A.close()
+
+
+def test_band_off_for_inverse_mode_and_long_restart(vk_lib, gpu):
+    p, A = _op(vk_lib, gpu, "S2")
+    M = vk_lib.block_jacobi(A, 8, mode="inverse")
+    b = coracle.rhs(p.n)
+    _, info, st = _solve(vk_lib, gpu, A, M, b, True)
+    assert info == 0 and st.band == 0
+    M.set_mode("auto")
+    _, info, st = _solve(vk_lib, gpu, A, M, b, True, restart=25)
+    assert info == 0 and st.band == 0
+    M.close()
+    A.close()
+
+
+def test_band_c1_vs_scipy_summary(vk_lib, gpu, golden_large):
+    """C1 against SciPy 1.15.3's own GMRES(20) + BJ(8) summary (golden_large.json)."""
+    g = golden_large["C1"]["gmres_bj8"]
+    p, A = _op(vk_lib, gpu, "C1")
+    M = vk_lib.block_jacobi(A, 8)
+    b = vk_lib.rhs_splitmix(p.n)
+    x, info, st = _solve(vk_lib, gpu, A, M, b, True)
+    assert st.band == 1
+    assert info == g["info"] == 0
+    assert abs(st.inner_iters - g["inner_iters"]) <= 1
+    assert np.linalg.norm(x) == pytest.approx(g["x_norm2"], rel=1e-9)
+    M.close()
+    A.close()

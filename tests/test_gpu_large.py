@@ -60,8 +60,8 @@ def _check(g, x, info, st, b, csr):
 @pytest.mark.parametrize("name", ["C2", "C3"])
 def test_gmres_full_size_vs_scipy(gpu, vk_lib, golden_large, name, path):
     p, x, info, st, b, csr, layout, mmode = _solve(vk_lib, gpu, name, path)
-    if path == "default":   # the bench's configuration, not a fallback
-        assert layout == "sell" and mmode == "tridiag" and st.orth == 1
+    if path == "default":   # the bench's configuration, not a fallback (line-band step included)
+        assert layout == "sell" and mmode == "tridiag" and st.orth == 1 and st.band == 1
     else:
         assert mmode == "inverse" and st.orth == 0
     _check(golden_large[name]["gmres_bj8"], x, info, st, b, csr)

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(vk_lib):
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(vk_lib._abi.PROTOTYPES), set(names) ^ set(vk_lib._abi.PROTOTYPES)
-    assert vk_lib._abi.lib().vtk_abi_version() == 1
+    assert vk_lib._abi.lib().vtk_abi_version() == 2
 
 
 def test_status_strings(vk_lib):

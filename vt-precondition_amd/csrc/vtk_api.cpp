@@ -615,6 +615,26 @@ void destroy_csr(vtk_csr *A) {
     delete A;
 }
 
+// line-band structure check (vtk_csr_set_line_band): VTK_OK when every column of every row lies
+// in the lines x-1..x+1 (mod X) of the row's line; VTK_ERR_ARG (no error text) otherwise
+int band_check(vtk_csr *A, int64_t L) {
+    vtk_ctx *c = A->ctx;
+    const int64_t n = A->n_local;
+    if (c->dist || L <= 0 || n % L != 0 || n / L < 3 || n / L > INT32_MAX || L > INT32_MAX ||
+        (double)(n + L) * (double)L >= 0x1p40)
+        return VTK_ERR_ARG;
+    DBuf bad;
+    TRY(dalloc(c, bad, sizeof(int)));
+    HIPCHK(c, hipMemsetAsync(bad.p, 0, sizeof(int), c->stream));
+    HIPCHK(c, launch_band_check(A->d_indptr, A->d_indices, n, (int)L, (int)(n / L), bad.as<int>(), c->stream));
+    int hb = 1;
+    HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (hb & 1) return VTK_ERR_ARG;
+    A->band_vloc = (hb & 2) == 0;
+    return VTK_OK;
+}
+
 // ---- GMRES -----------------------------------------------------------------------------------
 
 #ifndef VTK_DC_FUSED
@@ -635,6 +655,12 @@ struct Solver {
     double *Hraw = nullptr, *dcpart = nullptr;   // DCGS2
     DcCoef *cf = nullptr;
     double *x = nullptr;                         // the solution (the DCGS2 update pass may update it)
+    // line-band DCGS2 step (k_band_step): grid, w double buffer (s.w / s.tmp by step parity),
+    // first/last-line copies of p per workgroup (two sets, by step parity)
+    bool band = false;
+    int band_G = 0, band_H = 1;
+    double *edge[2] = {nullptr, nullptr};
+    double *vedge[2] = {nullptr, nullptr};   // per-line part-boundary rows of p (band_H > 1)
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
@@ -716,6 +742,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                    c->d_stop, c->stream));
         return VTK_OK;
     };
+    const bool band = s.band;
     bool broke = false;
     static const int ev_every = [] {
         const char *e = std::getenv("VTK_EV_EVERY");
@@ -728,7 +755,11 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *pj = s.V + (size_t)j * s.ld;
         int cnt = 0;
         const double b_step = b_csr + b_inv + n8 * (j + 2);   // CSR, BJ, p, w, V_j
-        if (fused && bj_split(s.M)) {
+        // band: step j's w and partials come from the band step j-1 (w alternates s.w / s.tmp)
+        double *w_cur = (band && (j & 1)) ? s.tmp : s.w;
+        if (band && j > 0) {
+            cnt = s.band_G;
+        } else if (fused && bj_split(s.M)) {
             // interior tiles while the halo is in flight, boundary tiles once it has landed;
             // their partials side by side (cnt = both grids)
             SpmvIn in = split_in(s.A, s.M, pj, true), bd = split_in(s.A, s.M, pj, false);
@@ -773,10 +804,42 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
         }
-        TRY(reduce_step(j, s.w, j, cnt));
-        { Prof pf(c, "dc_update", j, n8 * (j + 4));
-          HIPCHK(c, launch_dc_update(s.V, s.ld, j, s.w, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
-                                     c->stream)); }
+        TRY(reduce_step(j, w_cur, j, cnt));
+        if (band && j <= m - 2) {
+            // update pass of step j + SpMV, BJ and dots of step j+1 in one sweep over the x-lines
+            Prof pf(c, "band_step", j, b_csr + b_inv + n8 * (j + 6));   // V_j, p_j, w_j, v_j, p_j+1, w_j+1
+            BandK a;
+            a.pk = s.A->sell.d_pk;
+            a.dict = s.A->sell.d_dict;
+            a.val = static_cast<const double *>(s.A->sell.d_val);
+            a.mtri = s.M->d_tri + s.M->tri_ld;
+            a.V = s.V;
+            a.ld = s.ld;
+            a.j = j;
+            a.m = m;
+            a.w_in = w_cur;
+            a.w_out = (j & 1) ? s.w : s.tmp;
+            a.cf = s.cf;
+            a.st = ds;
+            a.x = s.x;
+            a.H = s.H;
+            a.S = s.S;
+            a.edge_in = s.edge[j & 1];
+            a.edge_out = s.edge[(j + 1) & 1];
+            a.vedge_in = s.vedge[j & 1];
+            a.vedge_out = s.vedge[(j + 1) & 1];
+            a.part = s.dcpart;
+            a.n = n;
+            a.L = (int)s.A->band_L;
+            a.X = (int)(n / s.A->band_L);
+            a.H_parts = s.band_H;
+            a.lmagic = (uint64_t)((((uint64_t)1 << 40) + (uint64_t)s.A->band_L - 1) / (uint64_t)s.A->band_L);
+            HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
+        } else {
+            Prof pf(c, "dc_update", j, n8 * (j + 4));
+            HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
+                                       c->stream));
+        }
         // throttle: an event every EV_EVERY steps (each record costs the stream a few us); the
         // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
         // has passed there.  Column cc stops in step cc (early commit) or cc+1: act only once
@@ -816,7 +879,30 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const bool dc = c->orth == VTK_ORTH_DCGS2 || (c->orth == VTK_ORTH_AUTO && m <= DC_MAXJ);
     if (dc && m > DC_MAXJ) return fail(c, VTK_ERR_ARG, "DCGS2 supports restart <= 32 (use VTK_ORTH_MGS)");
     const size_t ndc = dc ? (size_t)(m + 1) * (m + 1) + sizeof(DcCoef) / 8 + 8 + (size_t)DC_NQ * GMAX : 0;
-    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc;
+    // line-band DCGS2 step: one rank, SELL of uniform width 5 with coded columns (no wide chunk),
+    // f64 values, tridiagonal BJ(8) (the fused step's TRIM apply), restart <= 20
+    static const bool band_env = [] { const char *e = std::getenv("VTK_BAND"); return !(e && e[0] == '0'); }();
+    s.band = dc && band_env && c->band && !c->dist && A->band_L > 0 && A->band_L <= 800 && A->band_L % 8 == 0 &&
+             A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
+             M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_fused(M) && bj_op(M).tri != nullptr && m >= 2 && m <= 20;
+    int band_R = 0;
+    if (s.band) {
+        // parts per line (rows per workgroup <= 400; > 1 needs the v-locality of the couplings),
+        // two workgroups per CU, >= 2 lines per range
+        const int64_t X = n / A->band_L;
+        s.band_H = band_parts(A->band_L);
+        if (s.band_H < 1 || (s.band_H > 1 && !A->band_vloc)) s.band = false;
+        else {
+            const int64_t wg = (int64_t)band_wg_per_cu() * (c->n_cu > 0 ? c->n_cu : 256);
+            band_R = (int)std::min<int64_t>({wg / s.band_H, X / 2, (int64_t)GMAX / s.band_H});
+            s.band_G = band_R * s.band_H;
+            if (band_R < 1) s.band = false;
+        }
+    }
+    const size_t nedge1 = s.band ? (size_t)band_R * 2 * A->band_L : 0;
+    const size_t nvedge1 = s.band ? (size_t)(n / A->band_L) * s.band_H * 2 : 0;
+    const size_t nedge = 2 * (nedge1 + nvedge1);
+    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge + 8;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
         c->ws = nullptr;
@@ -837,7 +923,15 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         s.dcpart = wp; wp += (size_t)DC_NQ * GMAX;
         s.Hraw = wp; wp += (size_t)(m + 1) * (m + 1);
         s.cf = reinterpret_cast<DcCoef *>(wp);
+        wp += sizeof(DcCoef) / 8 + 8;
         HIPCHK(c, hipMemsetAsync(s.Hraw, 0, (size_t)(m + 1) * (m + 1) * sizeof(double), c->stream));
+    }
+    if (s.band) {
+        s.edge[0] = wp;
+        s.edge[1] = wp + nedge1;
+        s.vedge[0] = wp + 2 * nedge1;
+        s.vedge[1] = wp + 2 * nedge1 + nvedge1;
+        wp += nedge;
     }
     HIPCHK(c, hipMemsetAsync(s.H, 0, (size_t)m * (m + 1) * sizeof(double), c->stream));
     HIPCHK(c, hipMemsetAsync(s.giv, 0, (size_t)2 * m * sizeof(double), c->stream));
@@ -917,6 +1011,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     st.bnorm = bnrm2;
     st.atol_eff = atol;
     st.orth = dc ? VTK_ORTH_DCGS2 : VTK_ORTH_MGS;
+    st.band = s.band ? 1 : 0;
     auto done = [&](int inf) {
         *info = inf;
         st.t_solve = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -1002,10 +1097,10 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             if (hs->xup_tag >= 0) {
                 // the x update ran in update pass xup_tag: account it as the "xupdate" class and
                 // drop the host-enqueued k_xupdate (it returned at entry)
-                const int cu = prof_class(c, "dc_update"), cx = prof_class(c, "xupdate");
+                const int cu = prof_class(c, "dc_update"), cb = prof_class(c, "band_step"), cx = prof_class(c, "xupdate");
                 for (size_t i = 0; i < xup_idx && i < c->prof_pending.size(); ++i) {
                     auto &p = c->prof_pending[i];
-                    if (p.cls == cu && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
+                    if ((p.cls == cu || p.cls == cb) && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
                 }
                 if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].col = BIG_COL;
             }
@@ -1066,6 +1161,7 @@ int vtk_ctx_create(int device, vtk_ctx **out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return bad(e);
+    if ((e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess) return bad(e);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e);
     if ((e = hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking)) != hipSuccess) return bad(e);
     if ((e = hipEventCreateWithFlags(&c->ev_pack, hipEventDisableTiming)) != hipSuccess) return bad(e);
@@ -1264,6 +1360,8 @@ int vtk_csr_create_vlasov(vtk_ctx *c, const vtk_vlasov_params *p, const int64_t 
     HIPCHK(c, hipMalloc(&A->d_data, std::max<int64_t>(A->nnz, 1) * vb));
     HIPCHK(c, launch_vlasov_fill(*p, A->row_begin, nl, A->d_indptr, A->d_indices, A->d_data, c->stream));
     TRY(finish_csr(A));
+    // the 2D operator's rows form x-lines of Nv rows coupled to the neighbouring lines only
+    if (p->dim == 2 && !c->dist && band_check(A, p->shape[1]) == VTK_OK) A->band_L = p->shape[1];
     *out = A;
     A = nullptr;
     return VTK_OK;
@@ -1572,6 +1670,35 @@ void vtk_prec_destroy(vtk_prec *M) {
     free_tiles(M->tiles_in);
     free_tiles(M->tiles_bd);
     delete M;
+}
+
+int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len) {
+    if (!A) return fail(nullptr, VTK_ERR_ARG, "vtk_csr_set_line_band: A is NULL");
+    vtk_ctx *c = A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (line_len == 0) {
+        A->band_L = 0;
+        return VTK_OK;
+    }
+    const int rc = band_check(A, line_len);
+    if (rc == VTK_ERR_ARG)
+        return fail(c, VTK_ERR_ARG, "vtk_csr_set_line_band: not a line-band operator for this line length "
+                                    "(one rank, line_len | n, >= 3 lines, every column in lines x-1..x+1)");
+    TRY(rc);
+    A->band_L = line_len;
+    return VTK_OK;
+}
+
+int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len) {
+    if (!A || !line_len) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_csr_get_line_band: NULL argument");
+    *line_len = A->band_L;
+    return VTK_OK;
+}
+
+int vtk_gmres_set_band(vtk_ctx *c, int on) {
+    if (!c) return fail(nullptr, VTK_ERR_ARG, "vtk_gmres_set_band: ctx is NULL");
+    c->band = on != 0;
+    return VTK_OK;
 }
 
 int vtk_gmres_set_orth(vtk_ctx *c, int orth) {

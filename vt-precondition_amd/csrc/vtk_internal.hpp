@@ -126,6 +126,8 @@ struct vtk_ctx {
     bool host_comm = false;               // host-staged hooks (vtk_comm_init_host)
     vtk_host_comm hops{};
     int orth = VTK_ORTH_AUTO;
+    bool band = true;                     // line-band DCGS2 step allowed (vtk_gmres_set_band)
+    int n_cu = 0;                         // compute units (band step grid)
     // scratch shared by calls on this context
     double *d_part = nullptr;        // [8][GMAX] partial sums
     double *d_scal = nullptr;        // [256] reduced scalars (all-reduce slots)
@@ -168,6 +170,8 @@ struct vtk_csr {
     int32_t *d_send_idx = nullptr;                      // local rows to pack
     double *d_send_buf = nullptr;
     int64_t n_send = 0;
+    int64_t band_L = 0;                                 // line-band structure (vtk_csr_set_line_band)
+    bool band_vloc = false;                             // ... with every column within v-1..v+1 of its row
 };
 
 struct vtk_prec {
@@ -327,6 +331,41 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
                             const DcCoef *cf, int grid, const GmresState *st, double *x,
                             const double *H, const double *S, int m, int nt_pw, hipStream_t s);
+
+// Line-band DCGS2 step (k_band_step): update pass of step j + SpMV, tridiagonal BJ(8) and
+// dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded columns,
+// fp64 values; single rank).  grid workgroups (<= X lines, <= GMAX), partials of step j+1 in
+// the launch_dc_dots layout; edge_in / edge_out: [grid][2][L] first/last-line copies of p.
+struct BandK {
+    const uint32_t *pk;
+    const int32_t *dict;
+    const double *val;
+    const double *mtri;
+    double *V;
+    int64_t ld;
+    int j, m;
+    const double *w_in;
+    double *w_out;
+    const DcCoef *cf;
+    const GmresState *st;
+    double *x;
+    const double *H, *S;
+    const double *edge_in;       // [R][2][L]: first / last line of each line range (p of step j)
+    double *edge_out;
+    const double *vedge_in;      // [X][H][2]: first / last row of each line part (H > 1)
+    double *vedge_out;
+    double *part;
+    int64_t n;
+    int L, X, H_parts;           // line length, lines, parts per line (grid = ranges x H_parts)
+    uint64_t lmagic;   // floor(c / L) = (c * lmagic) >> 40 for c < 2^40 / L
+};
+hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
+int band_wg_per_cu();         // band step workgroups per CU
+int band_parts(int64_t L);    // parts per line (rows per part <= 400, multiple of 8); 0: none
+// *bad |= 1 when some column is outside the lines x-1..x+1 (mod X) of its row, |= 2 when one is
+// more than one row off its row's position in the line (bad zeroed by the caller)
+hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
+                             hipStream_t s);
 
 int vector_grid(int64_t n);
 

@@ -2761,13 +2761,13 @@ __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld
         rinv_s = cf->rinv;
     }
     if (c == j)
-        for (int k = threadIdx.x; k < j; k += NT) cs[k] = cf->s[k];
+        for (int k = threadIdx.x; k < j; k += blockDim.x) cs[k] = cf->s[k];
     __syncthreads();
     const double rinv = rinv_s;
     const double *pj = V + (size_t)j * ld;
     const int kv = c == j ? j : c + 1;   // stored basis vectors in the sum
-    const int64_t stride = 2 * (int64_t)gridDim.x * NT;
-    for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
+    const int64_t stride = 2 * (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += stride) {
         if (i + 1 < n) {
             double ax = 0.0, ay = 0.0;
             double2 a = make_double2(0.0, 0.0);
@@ -2896,6 +2896,271 @@ int vector_grid(int64_t n) {
     if (g < 1) g = 1;
     if (g > GMAX) g = GMAX;
     return (int)g;
+}
+
+
+// ------------------------------------------------------------------------------------------
+// Line-band DCGS2 step.  For an operator whose rows form x-lines of L rows
+// (row = x L + v) with every column in lines x-1, x, x+1 (periodic in x) at v-1..v+1 -- the 2D
+// Vlasov operators, L = Nv -- the update pass of step j and the fused SpMV + BJ + dots of step
+// j+1 run as ONE sweep.  Workgroup (range r, part h) owns rows v0 <= v < v0 + LP (LP = L / H)
+// of the lines [xa, xb) of range r and walks them in order; at line x it
+//   1. updates line x+1 (v_j, p_{j+1} exactly as k_dc_update) on its rows plus one v-halo row
+//      on each side, and puts p_{j+1}(x+1) into an LDS ring of 4 lines,
+//   2. computes w(x) = M^-1 A p_{j+1} on its rows of line x from the ring (the SELL entries in
+//      stored order and the tridiagonal BJ solve exactly as k_sell: w is bit-identical),
+//   3. accumulates step j+1's dots s = V_{j+1}^T p_{j+1}, z = V_{j+1}^T w, |p|^2, p.w, |w|^2
+//      from LDS: the line's basis rows were staged there by step 1 one line earlier.
+// The basis is read from HBM once per step instead of twice (update pass + dots), p_{j+1} is
+// never re-read for the SpMV gathers, and one launch replaces two.  Rows another workgroup owns
+// are recomputed: the x-halo lines xa-1 and xb (their p_j from the owner's copy of its first /
+// last line from the previous step -- the owner overwrites p_j in place with v_j) and the
+// v-halo rows v0-1, v0+LP (p_j from the owner's per-line boundary copies).  7 waves; lane
+// tid <-> row v = v0 - 8 + tid (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two
+// workgroups per CU, whose update / SpMV / dots phases overlap.
+// ------------------------------------------------------------------------------------------
+constexpr int BAND_LP = 400;   // max rows per workgroup part of a line
+constexpr int BAND_T = 448;    // threads per workgroup (7 waves): LP + 2 halo rows, lane-aligned
+constexpr int BAND_RS = 448;   // ring stride (rows v0-8 .. v0+LP+39 of a line)
+constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
+constexpr int BAND_W = BAND_T / 64;
+constexpr int BAND_IT = 3;     // dot items per wave (ceil(20 / 7))
+
+template <int WU, int J>
+__global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
+    __shared__ double vbuf[BAND_JV * BAND_LP];
+    __shared__ double ring[4 * BAND_RS];
+    __shared__ double wbuf[BAND_LP];
+    __shared__ double red[DC_NQ];
+    __shared__ double cs[BAND_JV], ce[BAND_JV];
+    constexpr int j = J;
+    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
+        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m);
+        return;
+    }
+    if (stopped(&a.st->stop_col, j)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int L = a.L, X = a.X, H = a.H_parts, LP = L / H;
+    const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
+    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
+    const int v = v0 - 8 + tid;
+    const bool own = tid >= 8 && tid < 8 + LP;
+    const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
+    const int ii = lane & 7;
+    for (int k = tid; k < j; k += BAND_T) {
+        cs[k] = a.cf->s[k];
+        ce[k] = a.cf->e[k];
+    }
+    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j];
+    __syncthreads();
+    double vreg[J + 1];
+    double acc[BAND_IT][3];
+#pragma unroll
+    for (int u = 0; u < BAND_IT; ++u) acc[u][0] = acc[u][1] = acc[u][2] = 0.0;
+    // update of line y on the lane's row: kind 0 an owned line, 1 / 2 the x-halo line before xa /
+    // after xb-1 (p_j from the owner's edge copy; nothing stored); owned lines' v-halo rows take
+    // p_j from the neighbour part's boundary copy.  vreg = V_k(y) k < j, then v_j.
+    auto update = [&](int y, int kind) -> double {
+        const int64_t row = (int64_t)y * L + (upd ? v : 0);
+        double pj = 0.0, wj = 0.0;
+        if (upd) {
+            if (j == 0 || (kind == 0 && own)) pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
+            else if (kind == 1) pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
+            else if (kind == 2) pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
+            else pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
+            wj = __builtin_nontemporal_load(a.w_in + row);
+        }
+#pragma unroll
+        for (int k = 0; k < J; ++k) vreg[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
+        double av = pj, tv = wj;
+#pragma unroll
+        for (int k = 0; k < J; ++k) {
+            const double sk = cs[k], ek = ce[k];
+            av = av - sk * vreg[k];
+            tv = tv - ek * vreg[k];
+        }
+        double vj = pj;
+        if (j >= 1) vj = av * rinv;
+        tv = tv - ej * vj;
+        const double pn = tv * qc;
+        vreg[J] = vj;
+        if (kind == 0 && own) {
+            if (j >= 1) __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+            __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
+            if (y == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
+            if (y == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
+            if (H > 1 && tid == 8) a.vedge_out[((size_t)y * H + h) * 2] = pn;
+            if (H > 1 && tid == 7 + LP) a.vedge_out[((size_t)y * H + h) * 2 + 1] = pn;
+        }
+        return pn;
+    };
+    auto stage = [&]() {
+        if (own) {
+#pragma unroll
+            for (int k = 0; k <= J; ++k) vbuf[k * BAND_LP + tid - 8] = vreg[k];
+        }
+    };
+    auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
+    // iteration it updates line y = xa - 1 + it (it = 0: the x-halo line before xa, it = nl + 1:
+    // the one after xb - 1) and, from it = 2 on, runs the SpMV and dots of line y - 1
+    const int nl = xb - xa;
+    for (int it = 0; it <= nl + 1; ++it) {
+        const int y = xa - 1 + it, x = y - 1;
+        const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
+        const int64_t lrow = (int64_t)(work ? x : xa) * L;
+        const int64_t row = lrow + (own ? v : v0);
+        // the SpMV operands of line x (independent of the update): codes, dictionary, values, m
+        const int64_t q = row >> 6, q0 = (lrow + v0 - 8 + 64 * wv) >> 6;
+        const int l64 = (int)(row & 63);
+        uint32_t word = 0u;
+        int dv = 0;
+        double d[WU];
+        double mrow = 1.0;
+        if (work) {
+            word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
+            const int64_t qd = q0 + (lane >> 4);
+            dv = (lane < 32 && qd >= 0 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
+#pragma unroll
+            for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
+            if (own) mrow = __builtin_nontemporal_load(a.mtri + row);
+        }
+        // 1. update of line y
+        {
+            const int kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
+            const int yy = it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : y);
+            const double pn = update(yy, kind);
+            if (upd) ring[slot(y) + tid] = pn;
+        }
+        __syncthreads();
+        if (work) {
+            // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
+            double sacc = 0.0, sub = 0.0, sup = 0.0;
+            const int sel = (int)(q - q0) * 16;
+#pragma unroll
+            for (int k = 0; k < WU; ++k) {
+                const int code = (int)((word >> (4 * k)) & 15u);
+                const int off = __shfl(dv, (sel + code) & 63, 64);
+                if (own && code != PK_CODES) {
+                    const int64_t c = row + off;
+                    const int64_t lc = (int64_t)(((uint64_t)c * a.lmagic) >> 40);
+                    int rel = (int)(lc - x);
+                    if (rel > 1) rel -= X;
+                    else if (rel < -1) rel += X;
+                    const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + (int)(c - lc * L) - v0 + 8];
+                    sacc += d[k] * xv;
+                    if (c == row - 1 && ii > 0) sub = sub + d[k];
+                    if (c == row + 1 && ii < 7) sup = sup + d[k];
+                }
+            }
+            const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
+            if (own) {
+                __builtin_nontemporal_store(z, a.w_out + row);
+                wbuf[tid - 8] = z;
+            }
+            __syncthreads();
+            // 3. dots of the part's rows of line x: wave wv owns items wv, wv + 7, wv + 14 (item
+            //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows
+            const double *pr = ring + slot(x) + 8;
+#pragma unroll
+            for (int u = 0; u < BAND_IT; ++u) {
+                const int itm = wv + BAND_W * u;
+                if (itm <= j) {
+                    const double *vk = vbuf + itm * BAND_LP;
+                    for (int t = lane; t < LP; t += 64) {
+                        const double vv = vk[t];
+                        acc[u][0] += vv * pr[t];
+                        acc[u][1] += vv * wbuf[t];
+                    }
+                } else if (itm == j + 1) {
+                    for (int t = lane; t < LP; t += 64) {
+                        const double pv = pr[t], wq = wbuf[t];
+                        acc[u][0] += pv * pv;
+                        acc[u][1] += pv * wq;
+                        acc[u][2] += wq * wq;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (it >= 1 && it <= nl) stage();   // line y is owned: its basis rows for the dots one line on
+    }
+    // per-workgroup partials in launch_dc_dots' layout for step j+1
+#pragma unroll
+    for (int u = 0; u < BAND_IT; ++u) {
+        const int itm = wv + BAND_W * u;
+        if (itm <= j + 1) {   // wave-uniform
+            const double t0 = wave_allsum(acc[u][0]), t1 = wave_allsum(acc[u][1]), t2 = wave_allsum(acc[u][2]);
+            if (lane == 0) {
+                if (itm <= j) {
+                    red[itm] = t0;
+                    red[DC_MAXJ + itm] = t1;
+                } else {
+                    red[2 * DC_MAXJ] = t0;
+                    red[2 * DC_MAXJ + 1] = t1;
+                    red[2 * DC_MAXJ + 2] = t2;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int jn = j + 1;
+    for (int qq = tid; qq < DC_NQ; qq += BAND_T) {
+        const bool used = qq < jn || (qq >= DC_MAXJ && qq < DC_MAXJ + jn) || qq >= 2 * DC_MAXJ;
+        if (used) a.part[(size_t)qq * GMAX + b] = red[qq];
+    }
+}
+
+int band_wg_per_cu() { return 2; }
+int band_parts(int64_t L) {
+    for (int h = 1; h <= 8; ++h)
+        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= BAND_LP) return h;
+    return 0;
+}
+
+hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
+    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > BAND_LP || (a.L / a.H_parts) % 8 != 0 ||
+        a.j + 1 > BAND_JV || grid < a.H_parts || grid > GMAX || grid % a.H_parts != 0 || grid / a.H_parts > a.X)
+        return hipErrorInvalidValue;
+    switch (a.j) {
+#define VTK_BAND_J(J_) case J_: hipLaunchKernelGGL((k_band_step<5, J_>), dim3(grid), dim3(BAND_T), 0, s, a); break;
+        VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
+        VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
+        VTK_BAND_J(14) VTK_BAND_J(15) VTK_BAND_J(16) VTK_BAND_J(17) VTK_BAND_J(18)
+#undef VTK_BAND_J
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// *bad |= 1 when a column lies outside lines x-1..x+1 (mod X) of its row's line x; |= 2 when it
+// lies more than one row off the row's position v within its line
+__global__ __launch_bounds__(NT) void k_band_check(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
+                                                   int64_t n, int L, int X, int *bad) {
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
+        const int64_t x = r / L, vr = r % L;
+        bool ok = true, vloc = true;
+        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
+            const int64_t c = indices[k];
+            if (c < 0 || c >= n) { ok = false; break; }
+            int64_t rel = c / L - x;
+            if (rel > 1) rel -= X;
+            else if (rel < -1) rel += X;
+            if (rel < -1 || rel > 1) { ok = false; break; }
+            const int64_t dv = c % L - vr;
+            if (dv < -1 || dv > 1) vloc = false;
+        }
+        if (!ok) atomicOr(bad, 1);
+        if (!vloc) atomicOr(bad, 2);
+    }
+}
+
+hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
+                             hipStream_t s) {
+    int64_t g = (n + NT - 1) / NT;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_band_check, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, X, bad);
+    return hipGetLastError();
 }
 
 }  // namespace vtk

@@ -144,6 +144,13 @@ class Context:
         check(lib().vtk_gmres_set_orth(self._h, int(orth)), self._h)
         self.orth = int(orth)
 
+    band = True
+
+    def set_band(self, on: bool):
+        """Allow (default) or forbid the line-band DCGS2 step (see csr_matrix.set_line_band)."""
+        check(lib().vtk_gmres_set_band(self._h, 1 if on else 0), self._h)
+        self.band = bool(on)
+
     def close(self):
         if getattr(self, "_h", None):
             lib().vtk_ctx_destroy(self._h)
@@ -198,6 +205,20 @@ class CsrOperator:
         v = C.c_int()
         check(lib().vtk_csr_get_layout(self._h, C.byref(v)), self.ctx.handle)
         return {1: "csr", 2: "sell", 3: "sell32"}[v.value]
+
+    def set_line_band(self, line_len: int):
+        """Declare the line-band structure: rows form x-lines of ``line_len`` rows and every
+        column lies in the lines x-1..x+1 (periodic) of its row's line (checked on the device;
+        0 clears it).  The 2D Vlasov operators get it automatically (line_len = Nv).  gmres then
+        fuses each DCGS2 update pass with the next step's SpMV + BJ + dots (one basis read per
+        step); results stay within the DCGS2 bars."""
+        check(lib().vtk_csr_set_line_band(self._h, int(line_len)), self.ctx.handle)
+
+    @property
+    def line_band(self) -> int:
+        v = C.c_int64()
+        check(lib().vtk_csr_get_line_band(self._h, C.byref(v)), self.ctx.handle)
+        return v.value
 
     def layout_info(self) -> dict:
         """Layout in use, bytes of the operator one SpMV reads in it, SELL chunk counts."""
@@ -512,6 +533,7 @@ class SolveStats:
     bytes_moved: float
     breakdown: int
     orth: int
+    band: int = 0   # 1: the line-band DCGS2 step ran
 
 
 _last_stats: SolveStats | None = None

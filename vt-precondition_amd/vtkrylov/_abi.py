@@ -41,7 +41,7 @@ class Stats(C.Structure):
     _fields_ = [("inner_iters", C.c_int64), ("restarts", C.c_int64), ("presid", C.c_double),
                 ("rnorm", C.c_double), ("bnorm", C.c_double), ("atol_eff", C.c_double),
                 ("t_solve", C.c_double), ("bytes_moved", C.c_double), ("breakdown", C.c_int),
-                ("orth", C.c_int)]
+                ("orth", C.c_int), ("band", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -85,6 +85,8 @@ PROTOTYPES = {
     "vtk_csr_set_layout": (C.c_int, [P, C.c_int]),
     "vtk_csr_get_layout": (C.c_int, [P, C.POINTER(C.c_int)]),
     "vtk_csr_layout_info": (C.c_int, [P, C.c_void_p]),
+    "vtk_csr_set_line_band": (C.c_int, [P, C.c_int64]),
+    "vtk_csr_get_line_band": (C.c_int, [P, I64P]),
     "vtk_bjacobi_get_mode": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_destroy": (None, [P]),
     "vtk_linejacobi_create": (C.c_int, [P, C.c_int64, C.c_int64, C.POINTER(P)]),
@@ -96,6 +98,7 @@ PROTOTYPES = {
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
                             C.POINTER(C.c_int), C.POINTER(Stats)]),
     "vtk_gmres_set_orth": (C.c_int, [P, C.c_int]),
+    "vtk_gmres_set_band": (C.c_int, [P, C.c_int]),
     "vtk_profile_enable": (C.c_int, [P, C.c_int]),
     "vtk_profile_read": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_int)]),
 }
@@ -138,7 +141,7 @@ def lib() -> C.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.vtk_abi_version() != 1:
+        if L.vtk_abi_version() != 2:
             raise ImportError("libvtkrylov.so ABI version mismatch")
         _lib = L
     return _lib
