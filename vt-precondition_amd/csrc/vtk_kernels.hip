@@ -2919,16 +2919,27 @@ int vector_grid(int64_t n) {
 // tid <-> row v = v0 - 8 + tid (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two
 // workgroups per CU, whose update / SpMV / dots phases overlap.
 // ------------------------------------------------------------------------------------------
-constexpr int BAND_LP = 400;   // max rows per workgroup part of a line
-constexpr int BAND_T = 448;    // threads per workgroup (7 waves): LP + 2 halo rows, lane-aligned
-constexpr int BAND_RS = 448;   // ring stride (rows v0-8 .. v0+LP+39 of a line)
 constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
-constexpr int BAND_W = BAND_T / 64;
-constexpr int BAND_IT = 3;     // dot items per wave (ceil(20 / 7))
+// geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
+// 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU)
+template <int GEO> struct BandGeo;
+template <> struct BandGeo<2> { static constexpr int LP = 400, T = 448, WPC = 2; };
+template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4; };
+#ifndef VTK_BAND_GEO
+#define VTK_BAND_GEO 2
+#endif
+#ifndef VTK_BAND_PF
+#define VTK_BAND_PF 8   // j <= this: next line's update operands prefetched across SpMV + dots
+#endif
+#ifndef VTK_BAND_VBUF_FIXED
+#define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
+#endif
 
-template <int WU, int J>
-__global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
-    __shared__ double vbuf[BAND_JV * BAND_LP];
+template <int WU, int J, int GEO>
+__global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
+    constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
+    constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
+    __shared__ double vbuf[(VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
     __shared__ double ring[4 * BAND_RS];
     __shared__ double wbuf[BAND_LP];
     __shared__ double red[DC_NQ];
@@ -2960,26 +2971,50 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) voi
     // update of line y on the lane's row: kind 0 an owned line, 1 / 2 the x-halo line before xa /
     // after xb-1 (p_j from the owner's edge copy; nothing stored); owned lines' v-halo rows take
     // p_j from the neighbour part's boundary copy.  vreg = V_k(y) k < j, then v_j.
-    auto update = [&](int y, int kind) -> double {
+    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1)
+    const int nl = xb - xa;
+    auto line_of = [&](int it, int &kind) {
+        kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
+        return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
+    };
+    // update operands of iteration it's line on the lane's row: V_k (k < j), p_j, w_j.  kind 1 / 2
+    // (x-halo lines): p_j from the owner's edge copy; owned lines' v-halo rows: p_j from the
+    // neighbour part's boundary copy (the owners overwrite p_j in place with v_j)
+    struct Ld {
+        double v[J > 0 ? J : 1];
+        double pj, wj;
+    };
+    auto load = [&](int it, Ld &o) {
+        int kind;
+        const int y = line_of(it, kind);
         const int64_t row = (int64_t)y * L + (upd ? v : 0);
-        double pj = 0.0, wj = 0.0;
+        o.pj = 0.0;
+        o.wj = 0.0;
         if (upd) {
-            if (j == 0 || (kind == 0 && own)) pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
-            else if (kind == 1) pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
-            else if (kind == 2) pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
-            else pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
-            wj = __builtin_nontemporal_load(a.w_in + row);
+            if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
+            else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
+            else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
+            else o.pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
+            o.wj = __builtin_nontemporal_load(a.w_in + row);
         }
 #pragma unroll
-        for (int k = 0; k < J; ++k) vreg[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
-        double av = pj, tv = wj;
+        for (int k = 0; k < J; ++k) o.v[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
+    };
+    // the update itself (k_dc_update's operations); stores on owned lines; vreg = V_k, v_j
+    auto update = [&](int it, const Ld &o) -> double {
+        int kind;
+        const int y = line_of(it, kind);
+        const int64_t row = (int64_t)y * L + (upd ? v : 0);
+#pragma unroll
+        for (int k = 0; k < J; ++k) vreg[k] = o.v[k];
+        double av = o.pj, tv = o.wj;
 #pragma unroll
         for (int k = 0; k < J; ++k) {
             const double sk = cs[k], ek = ce[k];
             av = av - sk * vreg[k];
             tv = tv - ek * vreg[k];
         }
-        double vj = pj;
+        double vj = o.pj;
         if (j >= 1) vj = av * rinv;
         tv = tv - ej * vj;
         const double pn = tv * qc;
@@ -3001,9 +3036,12 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) voi
         }
     };
     auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
-    // iteration it updates line y = xa - 1 + it (it = 0: the x-halo line before xa, it = nl + 1:
-    // the one after xb - 1) and, from it = 2 on, runs the SpMV and dots of line y - 1
-    const int nl = xb - xa;
+    // iteration it updates line y = xa - 1 + it and, from it = 2 on, runs the SpMV and dots of
+    // line y - 1.  PF (small j, registers allow): the next line's update operands are loaded
+    // during this line's SpMV and dots (software pipeline)
+    constexpr bool PF = J <= VTK_BAND_PF;
+    Ld nx;
+    if constexpr (PF) load(0, nx);
     for (int it = 0; it <= nl + 1; ++it) {
         const int y = xa - 1 + it, x = y - 1;
         const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
@@ -3026,10 +3064,14 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) voi
         }
         // 1. update of line y
         {
-            const int kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
-            const int yy = it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : y);
-            const double pn = update(yy, kind);
+            Ld cu;
+            if constexpr (PF) cu = nx;
+            else load(it, cu);
+            const double pn = update(it, cu);
             if (upd) ring[slot(y) + tid] = pn;
+            if constexpr (PF) {
+                if (it <= nl) load(it + 1, nx);
+            }
         }
         __syncthreads();
         if (work) {
@@ -3110,19 +3152,34 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
 }
 
-int band_wg_per_cu() { return 2; }
+static int band_geo() {
+    static const int g = [] {
+        const char *e = std::getenv("VTK_BAND_GEO");
+        const int v = e ? std::atoi(e) : VTK_BAND_GEO;
+        return v == 4 ? 4 : 2;
+    }();
+    return g;
+}
+int band_wg_per_cu() { return band_geo() == 4 ? BandGeo<4>::WPC : BandGeo<2>::WPC; }
 int band_parts(int64_t L) {
-    for (int h = 1; h <= 8; ++h)
-        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= BAND_LP) return h;
+    const int lp = band_geo() == 4 ? BandGeo<4>::LP : BandGeo<2>::LP;
+    for (int h = 1; h <= 16; ++h)
+        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= lp) return h;
     return 0;
 }
 
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
-    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > BAND_LP || (a.L / a.H_parts) % 8 != 0 ||
+    const int geo = band_geo();
+    const int lp = geo == 4 ? BandGeo<4>::LP : BandGeo<2>::LP;
+    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > lp || (a.L / a.H_parts) % 8 != 0 ||
         a.j + 1 > BAND_JV || grid < a.H_parts || grid > GMAX || grid % a.H_parts != 0 || grid / a.H_parts > a.X)
         return hipErrorInvalidValue;
     switch (a.j) {
-#define VTK_BAND_J(J_) case J_: hipLaunchKernelGGL((k_band_step<5, J_>), dim3(grid), dim3(BAND_T), 0, s, a); break;
+#define VTK_BAND_J(J_)                                                                                           \
+    case J_:                                                                                                     \
+        if (geo == 4) hipLaunchKernelGGL((k_band_step<5, J_, 4>), dim3(grid), dim3(BandGeo<4>::T), 0, s, a);    \
+        else hipLaunchKernelGGL((k_band_step<5, J_, 2>), dim3(grid), dim3(BandGeo<2>::T), 0, s, a);             \
+        break;
         VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
         VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
         VTK_BAND_J(14) VTK_BAND_J(15) VTK_BAND_J(16) VTK_BAND_J(17) VTK_BAND_J(18)
