@@ -2955,6 +2955,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
     const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
     const int v = v0 - 8 + tid;
+    const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
     const bool own = tid >= 8 && tid < 8 + LP;
     const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
     const int ii = lane & 7;
@@ -3083,15 +3084,19 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                 const int code = (int)((word >> (4 * k)) & 15u);
                 const int off = __shfl(dv, (sel + code) & 63, 64);
                 if (own && code != PK_CODES) {
-                    const int64_t c = row + off;
-                    const int64_t lc = (int64_t)(((uint64_t)c * a.lmagic) >> 40);
-                    int rel = (int)(lc - x);
-                    if (rel > 1) rel -= X;
-                    else if (rel < -1) rel += X;
-                    const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + (int)(c - lc * L) - v0 + 8];
+                    // the column's line relative to x and its position in that line, by range
+                    // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
+                    const int t = v + off;
+                    int rel, vc;
+                    if (t >= 0 && t < L) { rel = 0; vc = t; }
+                    else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
+                    else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
+                    else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
+                    else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
+                    const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
                     sacc += d[k] * xv;
-                    if (c == row - 1 && ii > 0) sub = sub + d[k];
-                    if (c == row + 1 && ii < 7) sup = sup + d[k];
+                    if (off == -1 && ii > 0) sub = sub + d[k];
+                    if (off == 1 && ii < 7) sup = sup + d[k];
                 }
             }
             const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
