@@ -43,6 +43,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
         A = vk.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=ctx, offsets=offs)
     else:           # device assembly of this rank's rows
         A = vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=ctx, offsets=offs)
+    if from_host and p.dim == 2:   # declared by hand on an uploaded CSR (auto on vlasov_operator)
+        A.set_line_band(p.shape[1])
     x = twin.rhs(p.n, seed=0xC0FFEE)
     y = A @ x[rb:re_]
     M = vk.block_jacobi(A, 8)
@@ -52,7 +54,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
     st = vk.last_stats()
     gip, gix, gd = A.download()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), y=y, inv=inv, x=xs, info=info,
-             iters=st.inner_iters, rb=rb, re=re_, halo=A.n_halo, gip=gip, gix=gix, gd=gd,
+             iters=st.inner_iters, rb=rb, re=re_, halo=A.n_halo, gip=gip, gix=gix, gd=gd, band=st.band,
+             line_band=A.line_band,
              errors=np.array(hc.errors, dtype=object).astype(str))
     dist.barrier()
     dist.destroy_process_group()
@@ -61,7 +64,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
 @pytest.mark.parametrize("case,world,from_host,orth", [("S2", 2, False, "mgs"), ("S4", 3, False, "dcgs2"),
                                                        ("S2", 3, True, "dcgs2"), ("S4", 2, "npz", "dcgs2"),
                                                        ("C1", 2, False, "mgs"),
-                                                       ("C1", 2, False, "dcgs2")])
+                                                       ("C1", 2, False, "dcgs2"), ("C1", 3, False, "dcgs2"),
+                                                       ("S2", 2, True, "dcgs2")])
 def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 
@@ -88,6 +92,9 @@ def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
         assert np.array_equal(z["gix"], ix[ip[rb]:ip[re_]])          # download maps back to global
         assert np.array_equal(z["y"], y_ref[rb:re_])                  # bitwise SpMV rows
         assert np.array_equal(z["inv"], inv_ref[rb // 8:(re_ + 7) // 8])
+        # 2D operators under DCGS2 run the line-band step across ranks (ghost lines exchanged)
+        expect_band = p.dim == 2 and orth == "dcgs2"
+        assert int(z["band"]) == int(expect_band), (int(z["band"]), int(z["line_band"]))
         assert int(z["info"]) == ref.info == 0
         assert abs(int(z["iters"]) - ref.inner_iters) <= 1
         xs[rb:re_] = z["x"]

@@ -617,21 +617,75 @@ void destroy_csr(vtk_csr *A) {
 
 // line-band structure check (vtk_csr_set_line_band): VTK_OK when every column of every row lies
 // in the lines x-1..x+1 (mod X) of the row's line; VTK_ERR_ARG (no error text) otherwise
+// Distributed operators (world > 1, or a one-rank communicator): the slab must hold whole lines
+// and its halo must be exactly the two neighbour lines (left: the line before the slab, right: the
+// one after it, periodic); the per-step ghost exchange layout is derived here.
+int band_check_dist(vtk_csr *A, int64_t L, bool &solo) {
+    vtk_ctx *c = A->ctx;
+    const int64_t n = A->n_local, Xg = A->n_global / L;
+    solo = A->n_halo == 0 && A->n_send == 0;
+    if (solo) return VTK_OK;   // no neighbour: the one-rank form (periodic wrap inside the slab)
+    if (A->n_global % L != 0 || A->row_begin % L != 0 || n < 2 * L || A->n_halo != 2 * L) return VTK_ERR_ARG;
+    const int64_t left = (A->row_begin / L - 1 + Xg) % Xg, right = (A->row_end / L) % Xg;
+    if (left == right) return VTK_ERR_ARG;
+    int64_t gl[2];
+    for (int b = 0; b < 2; ++b) {
+        gl[b] = A->halo_cols[(size_t)b * L] / L;
+        for (int64_t v = 0; v < L; ++v)
+            if (A->halo_cols[(size_t)(b * L + v)] != gl[b] * L + v) return VTK_ERR_ARG;
+    }
+    if (!((gl[0] == left && gl[1] == right) || (gl[0] == right && gl[1] == left))) return VTK_ERR_ARG;
+    A->band_lblk = gl[0] == left ? 0 : 1;
+    auto owner = [&](int64_t line) {
+        for (int q = 0; q < c->world; ++q)
+            if (A->offsets[q] <= line * L && line * L < A->offsets[q + 1]) return q;
+        return -1;
+    };
+    const int pl = owner(left), pr = owner(right);
+    if (pl < 0 || pr < 0 || pl == c->rank || pr == c->rank) return VTK_ERR_ARG;
+    A->band_peer[0] = pl;
+    A->band_peer[1] = pr;
+    // per peer: sends [my last line if it is my right neighbour][my first line if it is my left],
+    // receives [into the left ghost if it is my left neighbour][into the right ghost if my right]:
+    // a pair that is both (two ranks) matches last line -> left ghost, first line -> right ghost
+    const int W = c->world;
+    A->band_scnt.assign(W, 0);
+    A->band_soff.assign(W, 0);
+    A->band_rcnt.assign(W, 0);
+    A->band_roff.assign(W, 0);
+    int64_t so = 0, ro = 0;
+    for (int q = 0; q < W; ++q) {
+        A->band_soff[q] = so;
+        A->band_roff[q] = ro;
+        if (q == pr) { A->band_off_last = so; so += 3 * L; }
+        if (q == pl) { A->band_off_first = so; so += 3 * L; }
+        if (q == pl) { A->band_off_left = ro; ro += 3 * L; }
+        if (q == pr) { A->band_off_right = ro; ro += 3 * L; }
+        A->band_scnt[q] = so - A->band_soff[q];
+        A->band_rcnt[q] = ro - A->band_roff[q];
+    }
+    return VTK_OK;
+}
+
 int band_check(vtk_csr *A, int64_t L) {
     vtk_ctx *c = A->ctx;
     const int64_t n = A->n_local;
-    if (c->dist || L <= 0 || n % L != 0 || n / L < 3 || n / L > INT32_MAX || L > INT32_MAX ||
-        (double)(n + L) * (double)L >= 0x1p40)
+    if (L <= 0 || n % L != 0 || n / L < 2 || n / L > INT32_MAX || L > INT32_MAX || n + 2 * L >= INT32_MAX)
         return VTK_ERR_ARG;
+    bool solo = true;
+    if (c->dist && band_check_dist(A, L, solo) != VTK_OK) return VTK_ERR_ARG;
+    if (solo && n / L < 3) return VTK_ERR_ARG;
     DBuf bad;
     TRY(dalloc(c, bad, sizeof(int)));
     HIPCHK(c, hipMemsetAsync(bad.p, 0, sizeof(int), c->stream));
-    HIPCHK(c, launch_band_check(A->d_indptr, A->d_indices, n, (int)L, (int)(n / L), bad.as<int>(), c->stream));
+    if (solo) HIPCHK(c, launch_band_check(A->d_indptr, A->d_indices, n, (int)L, (int)(n / L), bad.as<int>(), c->stream));
+    else HIPCHK(c, launch_band_check_dist(A->d_indptr, A->d_indices, n, (int)L, A->band_lblk, bad.as<int>(), c->stream));
     int hb = 1;
     HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (hb & 1) return VTK_ERR_ARG;
     A->band_vloc = (hb & 2) == 0;
+    A->band_ghost = !solo;
     return VTK_OK;
 }
 
@@ -661,6 +715,7 @@ struct Solver {
     int band_G = 0, band_H = 1;
     double *edge[2] = {nullptr, nullptr};
     double *vedge[2] = {nullptr, nullptr};   // per-line part-boundary rows of p (band_H > 1)
+    double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
@@ -804,7 +859,24 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
         }
+        // distributed band step: the x-neighbours' edge lines of v_{j-1}, p_j, w_j travel to the
+        // ghost buffers on the comm stream (after this step's all-reduce in RCCL order, overlapping
+        // the scalar step); the band step waits for them
+        const bool ghost_x = band && s.ghost && j <= m - 2;
+        if (ghost_x) HIPCHK(c, hipEventRecord(c->ev_pack, c->stream));
         TRY(reduce_step(j, w_cur, j, cnt));
+        if (ghost_x) {
+            vtk_csr *A = s.A;
+            const int L = (int)A->band_L;
+            HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_pack, 0));
+            HIPCHK(c, launch_ghost_pack(s.V, s.ld, j, w_cur, n, L, s.gsend, A->band_off_first, A->band_off_last,
+                                        c->comm_stream));
+            TRY(comm_alltoallv(c, s.gsend, A->band_scnt, A->band_soff, s.grecv, A->band_rcnt, A->band_roff, ncclDouble,
+                               sizeof(double), c->comm_stream));
+            HIPCHK(c, launch_ghost_unpack(s.grecv, A->band_off_left, A->band_off_right, j, m, L, s.ghost, c->comm_stream));
+            HIPCHK(c, hipEventRecord(c->ev_halo, c->comm_stream));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+        }
         if (band && j <= m - 2) {
             // update pass of step j + SpMV, BJ and dots of step j+1 in one sweep over the x-lines
             Prof pf(c, "band_step", j, b_csr + b_inv + n8 * (j + 6));   // V_j, p_j, w_j, v_j, p_j+1, w_j+1
@@ -833,6 +905,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.L = (int)s.A->band_L;
             a.X = (int)(n / s.A->band_L);
             a.H_parts = s.band_H;
+            a.ghost = s.ghost;
+            a.left_blk = s.A->band_lblk;
             a.lmagic = (uint64_t)((((uint64_t)1 << 40) + (uint64_t)s.A->band_L - 1) / (uint64_t)s.A->band_L);
             HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
@@ -882,7 +956,8 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     // line-band DCGS2 step: one rank, SELL of uniform width 5 with coded columns (no wide chunk),
     // f64 values, tridiagonal BJ(8) (the fused step's TRIM apply), restart <= 20
     static const bool band_env = [] { const char *e = std::getenv("VTK_BAND"); return !(e && e[0] == '0'); }();
-    s.band = dc && band_env && c->band && !c->dist && A->band_L > 0 && A->band_L <= 800 && A->band_L % 8 == 0 &&
+    s.band = dc && band_env && c->band && A->band_L > 0 && A->band_L <= 800 && A->band_L % 8 == 0 &&
+             (!c->dist || !A->band_ghost || c->comm || c->host_comm) &&
              A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
              M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_fused(M) && bj_op(M).tri != nullptr && m >= 2 && m <= 20;
     int band_R = 0;
@@ -901,7 +976,8 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     }
     const size_t nedge1 = s.band ? (size_t)band_R * 2 * A->band_L : 0;
     const size_t nvedge1 = s.band ? (size_t)(n / A->band_L) * s.band_H * 2 : 0;
-    const size_t nedge = 2 * (nedge1 + nvedge1);
+    const size_t nghost = (s.band && A->band_ghost) ? (size_t)2 * (m + 2) * A->band_L + 12 * (size_t)A->band_L : 0;
+    const size_t nedge = 2 * (nedge1 + nvedge1) + nghost;
     const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge + 8;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
@@ -931,6 +1007,11 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         s.edge[1] = wp + nedge1;
         s.vedge[0] = wp + 2 * nedge1;
         s.vedge[1] = wp + 2 * nedge1 + nvedge1;
+        if (A->band_ghost) {
+            s.ghost = wp + 2 * (nedge1 + nvedge1);
+            s.gsend = s.ghost + (size_t)2 * (m + 2) * A->band_L;
+            s.grecv = s.gsend + 6 * (size_t)A->band_L;
+        }
         wp += nedge;
     }
     HIPCHK(c, hipMemsetAsync(s.H, 0, (size_t)m * (m + 1) * sizeof(double), c->stream));
@@ -1361,7 +1442,7 @@ int vtk_csr_create_vlasov(vtk_ctx *c, const vtk_vlasov_params *p, const int64_t 
     HIPCHK(c, launch_vlasov_fill(*p, A->row_begin, nl, A->d_indptr, A->d_indices, A->d_data, c->stream));
     TRY(finish_csr(A));
     // the 2D operator's rows form x-lines of Nv rows coupled to the neighbouring lines only
-    if (p->dim == 2 && !c->dist && band_check(A, p->shape[1]) == VTK_OK) A->band_L = p->shape[1];
+    if (p->dim == 2 && band_check(A, p->shape[1]) == VTK_OK) A->band_L = p->shape[1];
     *out = A;
     A = nullptr;
     return VTK_OK;
@@ -1683,7 +1764,8 @@ int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len) {
     const int rc = band_check(A, line_len);
     if (rc == VTK_ERR_ARG)
         return fail(c, VTK_ERR_ARG, "vtk_csr_set_line_band: not a line-band operator for this line length "
-                                    "(one rank, line_len | n, >= 3 lines, every column in lines x-1..x+1)");
+                                    "(line_len | n, >= 3 lines, every column in lines x-1..x+1; across ranks: "
+                                    "slabs of whole lines whose halo is the two neighbour lines)");
     TRY(rc);
     A->band_L = line_len;
     return VTK_OK;

@@ -172,6 +172,14 @@ struct vtk_csr {
     int64_t n_send = 0;
     int64_t band_L = 0;                                 // line-band structure (vtk_csr_set_line_band)
     bool band_vloc = false;                             // ... with every column within v-1..v+1 of its row
+    // distributed band step: the halo is two neighbour lines; peers and the alltoallv layout of
+    // the per-step ghost exchange (3 L doubles per side), -1 offsets: no such side
+    bool band_ghost = false;                            // band across ranks: per-step ghost exchange
+    int band_lblk = 0;
+    int band_peer[2] = {-1, -1};                        // left, right neighbour rank
+    std::vector<int64_t> band_scnt, band_soff, band_rcnt, band_roff;
+    int64_t band_off_first = -1, band_off_last = -1;    // send offsets of the first / last line
+    int64_t band_off_left = -1, band_off_right = -1;    // recv offsets of the left / right ghost
 };
 
 struct vtk_prec {
@@ -357,9 +365,18 @@ struct BandK {
     double *part;
     int64_t n;
     int L, X, H_parts;           // line length, lines, parts per line (grid = ranges x H_parts)
+    const double *ghost;         // distributed: [2][m+2][L] the left / right neighbour lines'
+                                 // v_k (k < j), p_j, w_j (k_ghost_unpack); null on one rank
+    int left_blk;                // halo block (0 / 1) holding the left neighbour line
     uint64_t lmagic;   // floor(c / L) = (c * lmagic) >> 40 for c < 2^40 / L
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
+hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
+                                  hipStream_t s);
+hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,
+                             int64_t off_first, int64_t off_last, hipStream_t s);
+hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
+                               double *ghost, hipStream_t s);
 int band_wg_per_cu();         // band step workgroups per CU
 int band_parts(int64_t L);    // parts per line (rows per part <= 400, multiple of 8); 0: none
 // *bad |= 1 when some column is outside the lines x-1..x+1 (mod X) of its row, |= 2 when one is

@@ -2991,15 +2991,29 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         const int64_t row = (int64_t)y * L + (upd ? v : 0);
         o.pj = 0.0;
         o.wj = 0.0;
+        // a rank's first / last line range: the x-halo line is a neighbour rank's line, whose
+        // V_k, p_j, w_j arrived in the ghost buffer (slots k, m, m + 1)
+        const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
+                               ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
         if (upd) {
-            if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
-            else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
-            else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
-            else o.pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
-            o.wj = __builtin_nontemporal_load(a.w_in + row);
+            if (gh) {
+                o.pj = gh[(size_t)a.m * L + v];
+                o.wj = gh[(size_t)(a.m + 1) * L + v];
+            } else {
+                if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
+                else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
+                else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
+                else o.pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
+                o.wj = __builtin_nontemporal_load(a.w_in + row);
+            }
         }
+        if (gh) {
 #pragma unroll
-        for (int k = 0; k < J; ++k) o.v[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
+            for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < J; ++k) o.v[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
+        }
     };
     // the update itself (k_dc_update's operations); stores on owned lines; vreg = V_k, v_j
     auto update = [&](int it, const Ld &o) -> double {
@@ -3088,7 +3102,12 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                     // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
                     const int t = v + off;
                     int rel, vc;
-                    if (t >= 0 && t < L) { rel = 0; vc = t; }
+                    const int c = x * L + t;
+                    if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
+                        const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
+                        rel = blk == a.left_blk ? -1 : 1;
+                        vc = kk - blk * L;
+                    } else if (t >= 0 && t < L) { rel = 0; vc = t; }
                     else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
                     else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
                     else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
@@ -3191,6 +3210,87 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
 #undef VTK_BAND_J
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// ghost exchange of the distributed band step: pack the rank's first / last line
+// of v_{j-1} (V[j-1]; V[0] at j = 0), p_j (V[j]) and w_j into send pieces of 3 L, unpack the
+// received pieces into the ghost slots (v_{j-1} -> slot j-1 when j >= 1, p_j -> m, w_j -> m+1)
+__global__ __launch_bounds__(NT) void k_ghost_pack(const double *__restrict__ V, int64_t ld, int j,
+                                                   const double *__restrict__ w, int64_t n, int L,
+                                                   double *__restrict__ sbuf, int64_t off_first, int64_t off_last) {
+    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
+        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
+        const int64_t off = side == 0 ? off_first : off_last;
+        if (off < 0) continue;
+        const int64_t row = (side == 0 ? 0 : n - L) + t;
+        const double val = vec == 0 ? V[(size_t)(j >= 1 ? j - 1 : 0) * ld + row]
+                                    : (vec == 1 ? V[(size_t)j * ld + row] : w[row]);
+        sbuf[off + r] = val;
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_ghost_unpack(const double *__restrict__ rbuf, int64_t off_left, int64_t off_right,
+                                                     int j, int m, int L, double *__restrict__ ghost) {
+    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
+        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
+        const int64_t off = side == 0 ? off_left : off_right;
+        if (off < 0 || (vec == 0 && j == 0)) continue;
+        const int slot = vec == 0 ? j - 1 : m + vec - 1;
+        ghost[((size_t)side * (m + 2) + slot) * L + t] = rbuf[off + r];
+    }
+}
+
+hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,
+                             int64_t off_first, int64_t off_last, hipStream_t s) {
+    hipLaunchKernelGGL(k_ghost_pack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, V, ld, j, w, n, L, sbuf, off_first,
+                       off_last);
+    return hipGetLastError();
+}
+
+hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
+                               double *ghost, hipStream_t s) {
+    hipLaunchKernelGGL(k_ghost_unpack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, rbuf, off_left, off_right, j, m, L,
+                       ghost);
+    return hipGetLastError();
+}
+
+// distributed form of the check (local column numbering; the halo is exactly two neighbour lines,
+// halo block lblk the left one): an owned column within lines x-1..x+1 of the row's line without
+// wrap, a halo column only from the first (left block) or last (right block) local line
+__global__ __launch_bounds__(NT) void k_band_check_dist(const int32_t *__restrict__ indptr,
+                                                        const int32_t *__restrict__ indices, int64_t n, int L,
+                                                        int lblk, int *bad) {
+    const int64_t X = n / L;
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
+        const int64_t x = r / L, vr = r % L;
+        bool ok = true, vloc = true;
+        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
+            const int64_t c = indices[k];
+            int64_t vc;
+            if (c < 0 || c >= n + 2 * L) { ok = false; break; }
+            if (c < n) {
+                const int64_t rel = c / L - x;
+                if (rel < -1 || rel > 1) { ok = false; break; }
+                vc = c % L;
+            } else {
+                const int64_t kk = c - n, blk = kk / L;
+                if ((blk == lblk && x != 0) || (blk != lblk && x != X - 1)) { ok = false; break; }
+                vc = kk % L;
+            }
+            if (vc - vr < -1 || vc - vr > 1) vloc = false;
+        }
+        if (!ok) atomicOr(bad, 1);
+        if (!vloc) atomicOr(bad, 2);
+    }
+}
+
+hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
+                                  hipStream_t s) {
+    int64_t g = (n + NT - 1) / NT;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_band_check_dist, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, lblk, bad);
     return hipGetLastError();
 }
 
