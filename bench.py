@@ -416,7 +416,7 @@ def main():
     n_loc, nnz_loc = A.n_local, A.nnz
     csr_matrix_bytes = (4 if fp32 else 8) * nnz_loc + 4 * nnz_loc + 4 * (n_loc + 1)
     d_matrix = csr_matrix_bytes - linfo["matrix_bytes"]
-    dom_csr = dk["bytes"] / dk["launches"] + (d_matrix if dom.startswith("spmv") else 0.0)
+    dom_csr = dk["bytes"] / dk["launches"] + (d_matrix if dom.startswith("spmv") or dom == "band_step" else 0.0)
     solve_bytes = sum(v["bytes"] for v in kprof.values())
     it_solve = int(round(iters / args.steps))
     m = args.restart

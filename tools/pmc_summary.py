@@ -28,6 +28,7 @@ import statistics
 
 CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv3 output (default
               # path: SELL-64 layout, tridiagonal-factor BJ(8), DCGS2; fp64 or fp32 values)
+    "band_step": r"void vtk::k_band_step<",
     "spmv_bj_dc": r"void vtk::k_sell<(double|float), false, 4, 8, true,",
     "spmv": r"void vtk::k_sell<(double|float), false, 0, 1, false,",
     "spmv_resid_bj": r"void vtk::k_sell<(double|float), false, 3, 8, true,",
