@@ -1512,8 +1512,15 @@ int vtk_spmv(vtk_csr *A, const double *x, double *y, int kind) {
     return VTK_OK;
 }
 
-int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
+int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) { return vtk_bjacobi_create_ex(A, bs, VTK_BJ_SETUP_EXACT, out); }
+
+int vtk_bjacobi_create_ex(vtk_csr *A, int bs, int setup, vtk_prec **out) {
     if (!A || !out || bs < 1 || bs > 64) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_bjacobi_create: block size must be in [1, 64]");
+    if (setup != VTK_BJ_SETUP_EXACT && setup != VTK_BJ_SETUP_MFMA && setup != VTK_BJ_SETUP_AUTO)
+        return fail(A->ctx, VTK_ERR_ARG, "vtk_bjacobi_create_ex: unknown setup");
+    if (setup == VTK_BJ_SETUP_AUTO) setup = bs == 32 ? VTK_BJ_SETUP_MFMA : VTK_BJ_SETUP_EXACT;
+    if (setup == VTK_BJ_SETUP_MFMA && bs != 16 && bs != 32)
+        return fail(A->ctx, VTK_ERR_ARG, "vtk_bjacobi_create_ex: the MFMA setup takes bs 16 or 32");
     vtk_ctx *c = A->ctx;
     *out = nullptr;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1530,7 +1537,17 @@ int vtk_bjacobi_create(vtk_csr *A, int bs, vtk_prec **out) {
     if (!pow2) TRY(dalloc(c, work, std::max<int64_t>(M->nb, 1) * bs * bs * sizeof(double)));
     const int init = INT32_MAX;
     HIPCHK(c, hipMemcpyAsync(sing.p, &init, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, launch_bj_setup(A->d_indptr, A->d_indices, A->d_data, A->fp32, A->n_local, bs, M->d_inv, sing.as<int>(), work.as<double>(), c->stream));
+    {
+        Prof pf(c, setup == VTK_BJ_SETUP_MFMA ? "bj_setup_mfma" : "bj_setup", -1,
+                (double)M->nb * bs * bs * 8.0 + matrix_bytes(A));
+        if (setup == VTK_BJ_SETUP_MFMA)
+            HIPCHK(c, launch_bj_setup_mfma(A->d_indptr, A->d_indices, A->d_data, A->fp32, A->n_local, bs, M->d_inv,
+                                           sing.as<int>(), c->stream));
+        else
+            HIPCHK(c, launch_bj_setup(A->d_indptr, A->d_indices, A->d_data, A->fp32, A->n_local, bs, M->d_inv,
+                                      sing.as<int>(), work.as<double>(), c->stream));
+    }
+    prof_flush(c);
     int sb = 0;
     HIPCHK(c, hipMemcpyAsync(&sb, sing.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -281,6 +281,10 @@ hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, co
 hipError_t launch_bj_setup(const int32_t *indptr, const int32_t *indices, const void *data,
                            int fp32, int64_t n, int bs, double *inv, int *d_singular,
                            double *work, hipStream_t s);
+// the same inverses for bs 16 / 32 by blocked Gauss-Jordan on the matrix cores (k_bj_setup_mfma;
+// agrees with launch_bj_setup to rounding, not bit for bit)
+hipError_t launch_bj_setup_mfma(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
+                                int bs, double *inv, int *d_singular, hipStream_t s);
 // w -= h v_k with h = reduce(hin); part_out = sum v_next*w (or sum w^2 if v_next == null)
 hipError_t launch_mgs(Red hin, double *hout, double *w, const double *vk, const double *vnext,
                       int64_t n, double *part_out, int grid, const int *stop_col, int col,

@@ -1924,6 +1924,165 @@ __global__ __launch_bounds__(NT) void k_bj_setup_generic(const int32_t *__restri
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Block-Jacobi setup on the matrix cores (bs 16, 32): blocked Gauss-Jordan with
+// partial pivoting, one wave per diagonal block, [A | I] (BS x 2BS) staged in LDS.  Per panel of
+// 4 columns the lanes (one per row) run the 4 pivot steps on the panel and on W (the transformed
+// unit vectors e_c, inserted at their step), which gives the panel's transform as I + U C^T
+// after the recorded row swaps; the rest of [A | I] is updated by  Q += U Q[C, :]  -- a rank-4
+// update: one v_mfma_f64_16x16x4f64 per 16x16 tile (operand maps checked by
+// tools/probe_mfma_f64.hip).  Pivots: the first row of largest |a| among the unpivoted rows, as
+// the scalar kernel; the rank-4 sums round differently from its rank-1 sequence, so the inverse
+// agrees to ~1e-15 relative, not bit for bit (a tolerance mode, VTK_BJ_SETUP_MFMA).
+// ------------------------------------------------------------------------------------------
+typedef double d4v __attribute__((ext_vector_type(4)));
+template <typename VT, int BS>
+__global__ __launch_bounds__(256) void k_bj_setup_mfma(const int32_t *__restrict__ indptr,
+                                                        const int32_t *__restrict__ indices,
+                                                        const VT *__restrict__ data, int64_t n, int64_t nb,
+                                                        double *__restrict__ inv, int *singular) {
+    constexpr int S = 2 * BS + 1;          // LDS row stride (odd: conflict-free column reads)
+    constexpr int RT = BS / 16, CT = 2 * BS / 16;
+    __shared__ double Ts[4][BS * S];
+    __shared__ double Ws[4][BS * 4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+    if (blk >= nb) return;                 // wave-uniform; no workgroup barrier below
+    double *T = Ts[wv];
+    double *W = Ws[wv];
+    // [A | I]: the block's rows (duplicates add, halo columns skipped), padding rows = identity
+    for (int e = lane; e < BS * 2 * BS; e += 64) {
+        const int r = e / (2 * BS), cc = e % (2 * BS);
+        T[r * S + cc] = cc == BS + r ? 1.0 : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < BS) {
+        const int64_t row = blk * BS + lane;
+        if (row >= n) {
+            T[lane * S + lane] = 1.0;
+        } else {
+            const int64_t c0 = blk * BS;
+            for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
+                if (indices[k] >= n) continue;
+                const int64_t cc = indices[k] - c0;
+                if (cc >= 0 && cc < BS) T[lane * S + cc] = T[lane * S + cc] + (double)data[k];
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    bool sing = false;
+    for (int c0 = 0; c0 < BS; c0 += 4) {
+        // panel: lane r < BS holds row r of the 4 panel columns and of W
+        double pr[4], wr[4];
+        int pv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pr[k] = lane < BS ? T[lane * S + c0 + k] : 0.0;
+            wr[k] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = c0 + k;
+            double best = (lane < BS && lane >= c) ? __builtin_fabs(pr[k]) : -1.0;
+            int bidx = lane;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const double ob = __shfl_xor(best, off, 64);
+                const int oi = __shfl_xor(bidx, off, 64);
+                if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+            }
+            if (best == 0.0) sing = true;
+            const int piv = bidx;
+            pv[k] = piv;
+            // swap rows c and piv of the panel and W
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double pc = __shfl(pr[q], c, 64), pp = __shfl(pr[q], piv, 64);
+                const double wc = __shfl(wr[q], c, 64), wp = __shfl(wr[q], piv, 64);
+                if (lane == c) { pr[q] = pp; wr[q] = wp; }
+                else if (lane == piv) { pr[q] = pc; wr[q] = wc; }
+            }
+            wr[k] = lane == c ? 1.0 : 0.0;   // e_c enters W at its step
+            const double d = __shfl(pr[k], c, 64);
+            if (lane == c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { pr[q] = pr[q] / d; wr[q] = wr[q] / d; }
+            }
+            const double f = pr[k];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double pcq = __shfl(pr[q], c, 64), wcq = __shfl(wr[q], c, 64);
+                if (lane != c) { pr[q] = pr[q] - f * pcq; wr[q] = wr[q] - f * wcq; }
+            }
+        }
+        // U = W - [e_c0 .. e_c0+3]
+        if (lane < BS) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) W[lane * 4 + k] = wr[k] - (lane == c0 + k ? 1.0 : 0.0);
+        }
+        // the panel's row swaps on the whole of [A | I] (Q = P [A | I])
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = c0 + k, piv = __builtin_amdgcn_readfirstlane(pv[k]);
+            __builtin_amdgcn_wave_barrier();
+            if (piv != c) {
+                for (int cc = lane; cc < 2 * BS; cc += 64) {
+                    const double a = T[c * S + cc], bb = T[piv * S + cc];
+                    T[c * S + cc] = bb;
+                    T[piv * S + cc] = a;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // Q += U Q[C, :]: the pivot rows (B operands) read before any tile is written
+        double bq[CT], ua[RT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) bq[ct] = T[(c0 + (lane >> 4)) * S + ct * 16 + (lane & 15)];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) ua[rt] = W[(rt * 16 + (lane & 15)) * 4 + (lane >> 4)];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                d4v acc;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = T[(rt * 16 + (lane >> 4) + 4 * i) * S + ct * 16 + (lane & 15)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua[rt], bq[ct], acc, 0, 0, 0);
+                const int col = ct * 16 + (lane & 15);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = rt * 16 + (lane >> 4) + 4 * i;
+                    // the panel columns are exactly e_C after their eliminations
+                    T[r * S + col] = (col >= c0 && col < c0 + 4) ? (r == col ? 1.0 : 0.0) : acc[i];
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (sing && lane == 0) atomicMin(singular, (int)blk);
+    double *o = inv + (size_t)blk * BS * BS;
+    for (int e = lane; e < BS * BS; e += 64) o[e] = T[(e / BS) * S + BS + e % BS];
+}
+
+template <typename VT>
+static hipError_t bj_setup_mfma_t(const int32_t *indptr, const int32_t *indices, const VT *data, int64_t n, int bs,
+                                  double *inv, int *sing, hipStream_t s) {
+    const int64_t nb = (n + bs - 1) / bs;
+    if (nb == 0) return hipSuccess;
+    const dim3 g((unsigned)((nb + 3) / 4));
+    if (bs == 16) hipLaunchKernelGGL((k_bj_setup_mfma<VT, 16>), g, dim3(256), 0, s, indptr, indices, data, n, nb, inv, sing);
+    else if (bs == 32) hipLaunchKernelGGL((k_bj_setup_mfma<VT, 32>), g, dim3(256), 0, s, indptr, indices, data, n, nb, inv, sing);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_bj_setup_mfma(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
+                                int bs, double *inv, int *d_singular, hipStream_t s) {
+    if (fp32) return bj_setup_mfma_t<float>(indptr, indices, static_cast<const float *>(data), n, bs, inv, d_singular, s);
+    return bj_setup_mfma_t<double>(indptr, indices, static_cast<const double *>(data), n, bs, inv, d_singular, s);
+}
+
 template <typename VT>
 static hipError_t bj_setup_t(const int32_t *indptr, const int32_t *indices, const VT *data, int64_t n,
                              int bs, double *inv, int *sing, double *work, hipStream_t s) {

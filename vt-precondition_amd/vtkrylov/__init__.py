@@ -362,13 +362,22 @@ class BlockJacobi:
     ``mode``: how M^-1 is applied (same operator either way): "inverse" multiplies by the
     block inverses (bit-identical to the oracle), "tridiag" solves with the LU factors of
     tridiagonal blocks (bs 2/4/8; 24 B/row instead of 8*bs), "auto" (default) takes "tridiag"
-    when every block is tridiagonal and its factors pass the setup check."""
+    when every block is tridiagonal and its factors pass the setup check.
 
-    def __init__(self, A: CsrOperator, bs: int = 8, mode: str = "auto"):
+    ``setup``: how the inverses are computed: "exact" (Gauss-Jordan with partial pivoting,
+    bit-identical to the oracle), "mfma" (bs 16 / 32: blocked Gauss-Jordan with the rank-4 panel
+    updates on the fp64 matrix cores; same pivot rule, rounding-level differences) or "auto"
+    (default: "mfma" for bs 32, where it is 4.5x faster, else "exact")."""
+
+    SETUPS = {"exact": 0, "mfma": 1, "auto": 2}
+
+    def __init__(self, A: CsrOperator, bs: int = 8, mode: str = "auto", setup: str = "auto"):
         if mode not in BJ_MODES:
             raise ValueError(f"mode must be one of {sorted(BJ_MODES)}")
+        if setup not in self.SETUPS:
+            raise ValueError(f"setup must be one of {sorted(self.SETUPS)}")
         h = C.c_void_p()
-        check(lib().vtk_bjacobi_create(A.handle, int(bs), C.byref(h)), A.ctx.handle)
+        check(lib().vtk_bjacobi_create_ex(A.handle, int(bs), self.SETUPS[setup], C.byref(h)), A.ctx.handle)
         self._h = h
         self.A = A
         self.bs = bs
@@ -429,8 +438,8 @@ class BlockJacobi:
             pass
 
 
-def block_jacobi(A: CsrOperator, bs: int = 8, mode: str = "auto") -> BlockJacobi:
-    return BlockJacobi(A, bs, mode)
+def block_jacobi(A: CsrOperator, bs: int = 8, mode: str = "auto", setup: str = "auto") -> BlockJacobi:
+    return BlockJacobi(A, bs, mode, setup)
 
 
 class LineJacobi:

@@ -99,6 +99,7 @@ PROTOTYPES = {
                             C.POINTER(C.c_int), C.POINTER(Stats)]),
     "vtk_gmres_set_orth": (C.c_int, [P, C.c_int]),
     "vtk_gmres_set_band": (C.c_int, [P, C.c_int]),
+    "vtk_bjacobi_create_ex": (C.c_int, [P, C.c_int, C.c_int, C.c_void_p]),
     "vtk_profile_enable": (C.c_int, [P, C.c_int]),
     "vtk_profile_read": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_int)]),
 }
