@@ -426,6 +426,22 @@ def main():
     sec8d = sum(B_spmv + B_pc + 8 * n_loc * (2 * (k % m) + 8) for k in range(it_solve)) \
         + cycles * (B_spmv + 24 * n_loc + B_pc + 24 * n_loc + 8 * n_loc * (m + 2))
     t_solve = ms / 1e3
+    # the band step does the work of the fused SpMV+BJ+dots kernel AND the update
+    # pass; those two would read the basis once more per launch (8 n j bytes).  Its algorithmic
+    # bytes per launch are matrix + m + 8 n (j + 6), so sum_j 8 n j = bytes - launches * (matrix
+    # + m + 48 n): the unfused-equivalent bytes and rate of the same work.
+    band_equiv = None
+    if "band_step" in kprof:
+        bk = kprof["band_step"]
+        fixed = linfo["matrix_bytes"] + 8.0 * n_loc + 48.0 * n_loc
+        extra = bk["bytes"] - bk["launches"] * fixed
+        eq = (bk["bytes"] + extra) / bk["launches"]
+        band_equiv = {"kernel": "band_step", "bytes_per_launch": bk["bytes"] / bk["launches"],
+                      "unfused_equiv_bytes_per_launch": eq, "avg_us": bk["avg_us"],
+                      "unfused_equiv_gbs": eq / (bk["avg_us"] * 1e-6) / 1e9,
+                      "unfused_equiv_frac": eq / (bk["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                      "note": "bytes the fused SpMV+BJ+dots kernel and the update pass would move for the "
+                              "same step (one more basis read) / the band step's time"}
     recon = {
         "note": "SURVEY 8(d) reconciliation; per rank (n_local rows); frac = GB/s / 8000",
         "dominant_kernel_csr_equiv": {"kernel": dom, "bytes_per_launch": dom_csr,
@@ -481,6 +497,7 @@ def main():
                      "algorithmic_bytes_per_launch": dk["bytes"] / dk["launches"],
                      "avg_us": dk["avg_us"], "launches": dk["launches"],
                      "share_of_solve": dk["seconds"] / tot_s},
+        "roofline_band_unfused_equiv": band_equiv,
         "roofline_spmv": {"kernel": f"spmv ({linfo['layout']}, vtk_spmv)", "bound": "hbm",
                           "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": spmv_gbs / HBM_PEAK_GBS, "traffic": traffic_spmv,

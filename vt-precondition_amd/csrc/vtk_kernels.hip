@@ -3087,8 +3087,11 @@ template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4;
 #ifndef VTK_BAND_GEO
 #define VTK_BAND_GEO 2
 #endif
+#ifndef VTK_BAND_REREAD
+#define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
+#endif
 #ifndef VTK_BAND_PF
-#define VTK_BAND_PF 8   // j <= this: next line's update operands prefetched across SpMV + dots
+#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 8)   // j <= this: next line's update operands prefetched across SpMV + dots
 #endif
 #ifndef VTK_BAND_VBUF_FIXED
 #define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
@@ -3098,7 +3101,7 @@ template <int WU, int J, int GEO>
 __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
     constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
-    __shared__ double vbuf[(VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
+    __shared__ double vbuf[VTK_BAND_REREAD ? 1 : (VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
     __shared__ double ring[4 * BAND_RS];
     __shared__ double wbuf[BAND_LP];
     __shared__ double red[DC_NQ];
@@ -3171,7 +3174,9 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
             for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
         } else {
 #pragma unroll
-            for (int k = 0; k < J; ++k) o.v[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
+            for (int k = 0; k < J; ++k)
+                o.v[k] = upd ? (VTK_BAND_REREAD ? a.V[(size_t)k * a.ld + row]
+                                                : __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row)) : 0.0;
         }
     };
     // the update itself (k_dc_update's operations); stores on owned lines; vreg = V_k, v_j
@@ -3194,7 +3199,10 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         const double pn = tv * qc;
         vreg[J] = vj;
         if (kind == 0 && own) {
-            if (j >= 1) __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+            if (j >= 1) {
+                if constexpr (VTK_BAND_REREAD) a.V[(size_t)j * a.ld + row] = vj;
+                else __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+            }
             __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
             if (y == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
             if (y == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
@@ -3204,7 +3212,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         return pn;
     };
     auto stage = [&]() {
-        if (own) {
+        if (!VTK_BAND_REREAD && own) {
 #pragma unroll
             for (int k = 0; k <= J; ++k) vbuf[k * BAND_LP + tid - 8] = vreg[k];
         }
@@ -3290,7 +3298,8 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
             for (int u = 0; u < BAND_IT; ++u) {
                 const int itm = wv + BAND_W * u;
                 if (itm <= j) {
-                    const double *vk = vbuf + itm * BAND_LP;
+                    const double *vk = VTK_BAND_REREAD ? a.V + (size_t)itm * a.ld + (int64_t)x * L + v0
+                                                       : vbuf + itm * BAND_LP;
                     for (int t = lane; t < LP; t += 64) {
                         const double vv = vk[t];
                         acc[u][0] += vv * pr[t];
