@@ -3087,6 +3087,9 @@ template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4;
 #ifndef VTK_BAND_GEO
 #define VTK_BAND_GEO 2
 #endif
+#ifndef VTK_BAND_DOTS_UNROLL
+#define VTK_BAND_DOTS_UNROLL 2   // the dots' 64-row passes issued together (LDS latency once per group)
+#endif
 #ifndef VTK_BAND_REREAD
 #define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
 #endif
@@ -3300,12 +3303,14 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                 if (itm <= j) {
                     const double *vk = VTK_BAND_REREAD ? a.V + (size_t)itm * a.ld + (int64_t)x * L + v0
                                                        : vbuf + itm * BAND_LP;
+#pragma unroll VTK_BAND_DOTS_UNROLL
                     for (int t = lane; t < LP; t += 64) {
                         const double vv = vk[t];
                         acc[u][0] += vv * pr[t];
                         acc[u][1] += vv * wbuf[t];
                     }
                 } else if (itm == j + 1) {
+#pragma unroll VTK_BAND_DOTS_UNROLL
                     for (int t = lane; t < LP; t += 64) {
                         const double pv = pr[t], wq = wbuf[t];
                         acc[u][0] += pv * pv;
