@@ -206,8 +206,8 @@ int vtk_bjacobi_create(vtk_csr *A, int block_size, vtk_prec **out);
 /* how the block inverses are computed: EXACT = Gauss-Jordan with partial pivoting, one lane per
  * block row, bit-identical to numpy.linalg.inv's oracle restatement; MFMA (bs 16 / 32 only) =
  * blocked Gauss-Jordan whose rank-4 panel updates run on v_mfma_f64_16x16x4f64 -- the same pivot
- * rule, rounding-level differences; AUTO = MFMA for bs 32 (4.5x faster at C3),
- * EXACT otherwise.  vtk_bjacobi_create uses EXACT. */
+ * rule, rounding-level differences; AUTO = MFMA for bs 16 and 32 (2.3x / 4.7x
+ * faster at C3), EXACT otherwise.  vtk_bjacobi_create uses EXACT. */
 typedef enum { VTK_BJ_SETUP_EXACT = 0, VTK_BJ_SETUP_MFMA = 1, VTK_BJ_SETUP_AUTO = 2 } vtk_bj_setup;
 int vtk_bjacobi_create_ex(vtk_csr *A, int block_size, int setup, vtk_prec **out);
 /* export the block inverses: (n_local + bs - 1) / bs blocks of bs*bs doubles, row-major */

@@ -1518,7 +1518,7 @@ int vtk_bjacobi_create_ex(vtk_csr *A, int bs, int setup, vtk_prec **out) {
     if (!A || !out || bs < 1 || bs > 64) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_bjacobi_create: block size must be in [1, 64]");
     if (setup != VTK_BJ_SETUP_EXACT && setup != VTK_BJ_SETUP_MFMA && setup != VTK_BJ_SETUP_AUTO)
         return fail(A->ctx, VTK_ERR_ARG, "vtk_bjacobi_create_ex: unknown setup");
-    if (setup == VTK_BJ_SETUP_AUTO) setup = bs == 32 ? VTK_BJ_SETUP_MFMA : VTK_BJ_SETUP_EXACT;
+    if (setup == VTK_BJ_SETUP_AUTO) setup = (bs == 16 || bs == 32) ? VTK_BJ_SETUP_MFMA : VTK_BJ_SETUP_EXACT;
     if (setup == VTK_BJ_SETUP_MFMA && bs != 16 && bs != 32)
         return fail(A->ctx, VTK_ERR_ARG, "vtk_bjacobi_create_ex: the MFMA setup takes bs 16 or 32");
     vtk_ctx *c = A->ctx;

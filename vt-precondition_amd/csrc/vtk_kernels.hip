@@ -1936,133 +1936,153 @@ __global__ __launch_bounds__(NT) void k_bj_setup_generic(const int32_t *__restri
 // agrees to ~1e-15 relative, not bit for bit (a tolerance mode, VTK_BJ_SETUP_MFMA).
 // ------------------------------------------------------------------------------------------
 typedef double d4v __attribute__((ext_vector_type(4)));
-template <typename VT, int BS>
+// NB blocks per wave: lane group g = lane / BS holds the rows of block g during the load and the
+// panel pivoting (bs 16: four blocks per wave, every lane busy); the MFMA tiles of the NB blocks
+// are issued back to back by the whole wave.
+template <typename VT, int BS, int NB>
 __global__ __launch_bounds__(256) void k_bj_setup_mfma(const int32_t *__restrict__ indptr,
                                                         const int32_t *__restrict__ indices,
                                                         const VT *__restrict__ data, int64_t n, int64_t nb,
                                                         double *__restrict__ inv, int *singular) {
     constexpr int S = 2 * BS + 1;          // LDS row stride (odd: conflict-free column reads)
     constexpr int RT = BS / 16, CT = 2 * BS / 16;
-    __shared__ double Ts[4][BS * S];
-    __shared__ double Ws[4][BS * 4];
+    static_assert(NB * BS <= 64, "one lane per block row");
+    __shared__ double Ts[4][NB][BS * S];
+    __shared__ double Ws[4][NB][BS * 4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t blk = (int64_t)blockIdx.x * 4 + wv;
-    if (blk >= nb) return;                 // wave-uniform; no workgroup barrier below
-    double *T = Ts[wv];
-    double *W = Ws[wv];
+    const int grp = lane / BS, r = lane % BS;
+    const bool gl = grp < NB;              // a lane of a block group
+    const int64_t blk0 = ((int64_t)blockIdx.x * 4 + wv) * NB;
+    if (blk0 >= nb) return;                // wave-uniform; no workgroup barrier below
+    const int64_t blk = blk0 + (gl ? grp : 0);
+    const bool live = gl && blk < nb;      // blocks past nb: identity, not stored
     // [A | I]: the block's rows (duplicates add, halo columns skipped), padding rows = identity
-    for (int e = lane; e < BS * 2 * BS; e += 64) {
-        const int r = e / (2 * BS), cc = e % (2 * BS);
-        T[r * S + cc] = cc == BS + r ? 1.0 : 0.0;
-    }
+    for (int g = 0; g < NB; ++g)
+        for (int e = lane; e < BS * 2 * BS; e += 64) {
+            const int rr = e / (2 * BS), cc = e % (2 * BS);
+            Ts[wv][g][rr * S + cc] = (cc == BS + rr || (blk0 + g >= nb && cc == rr)) ? 1.0 : 0.0;
+        }
     __builtin_amdgcn_wave_barrier();
-    if (lane < BS) {
-        const int64_t row = blk * BS + lane;
+    if (live) {
+        double *T = Ts[wv][grp];
+        const int64_t row = blk * BS + r;
         if (row >= n) {
-            T[lane * S + lane] = 1.0;
+            T[r * S + r] = 1.0;
         } else {
             const int64_t c0 = blk * BS;
             for (int k = indptr[row]; k < indptr[row + 1]; ++k) {
                 if (indices[k] >= n) continue;
                 const int64_t cc = indices[k] - c0;
-                if (cc >= 0 && cc < BS) T[lane * S + cc] = T[lane * S + cc] + (double)data[k];
+                if (cc >= 0 && cc < BS) T[r * S + cc] = T[r * S + cc] + (double)data[k];
             }
         }
     }
     __builtin_amdgcn_wave_barrier();
+    double *Tg = Ts[wv][gl ? grp : 0];
+    double *Wg = Ws[wv][gl ? grp : 0];
+    const int gb = (gl ? grp : 0) * BS;    // first lane of the group
     bool sing = false;
     for (int c0 = 0; c0 < BS; c0 += 4) {
-        // panel: lane r < BS holds row r of the 4 panel columns and of W
+        // panel: lane r of group g holds row r of block g's 4 panel columns and of W
         double pr[4], wr[4];
         int pv[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            pr[k] = lane < BS ? T[lane * S + c0 + k] : 0.0;
+            pr[k] = gl ? Tg[r * S + c0 + k] : 0.0;
             wr[k] = 0.0;
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = c0 + k;
-            double best = (lane < BS && lane >= c) ? __builtin_fabs(pr[k]) : -1.0;
-            int bidx = lane;
+            double best = (gl && r >= c) ? __builtin_fabs(pr[k]) : -1.0;
+            int bidx = r;
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
+            for (int off = 1; off < BS; off <<= 1) {
                 const double ob = __shfl_xor(best, off, 64);
                 const int oi = __shfl_xor(bidx, off, 64);
                 if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
             }
-            if (best == 0.0) sing = true;
+            if (best == 0.0 && live) sing = true;
             const int piv = bidx;
             pv[k] = piv;
-            // swap rows c and piv of the panel and W
+            // swap rows c and piv of the panel and W (within the group)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double pc = __shfl(pr[q], c, 64), pp = __shfl(pr[q], piv, 64);
-                const double wc = __shfl(wr[q], c, 64), wp = __shfl(wr[q], piv, 64);
-                if (lane == c) { pr[q] = pp; wr[q] = wp; }
-                else if (lane == piv) { pr[q] = pc; wr[q] = wc; }
+                const double pc = __shfl(pr[q], gb + c, 64), pp = __shfl(pr[q], gb + piv, 64);
+                const double wc = __shfl(wr[q], gb + c, 64), wp = __shfl(wr[q], gb + piv, 64);
+                if (r == c) { pr[q] = pp; wr[q] = wp; }
+                else if (r == piv) { pr[q] = pc; wr[q] = wc; }
             }
-            wr[k] = lane == c ? 1.0 : 0.0;   // e_c enters W at its step
-            const double d = __shfl(pr[k], c, 64);
-            if (lane == c) {
+            wr[k] = r == c ? 1.0 : 0.0;   // e_c enters W at its step
+            const double d = __shfl(pr[k], gb + c, 64);
+            if (r == c) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) { pr[q] = pr[q] / d; wr[q] = wr[q] / d; }
             }
             const double f = pr[k];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double pcq = __shfl(pr[q], c, 64), wcq = __shfl(wr[q], c, 64);
-                if (lane != c) { pr[q] = pr[q] - f * pcq; wr[q] = wr[q] - f * wcq; }
+                const double pcq = __shfl(pr[q], gb + c, 64), wcq = __shfl(wr[q], gb + c, 64);
+                if (r != c) { pr[q] = pr[q] - f * pcq; wr[q] = wr[q] - f * wcq; }
             }
         }
         // U = W - [e_c0 .. e_c0+3]
-        if (lane < BS) {
+        if (gl) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) W[lane * 4 + k] = wr[k] - (lane == c0 + k ? 1.0 : 0.0);
+            for (int k = 0; k < 4; ++k) Wg[r * 4 + k] = wr[k] - (r == c0 + k ? 1.0 : 0.0);
         }
-        // the panel's row swaps on the whole of [A | I] (Q = P [A | I])
+        // the panel's row swaps on the whole of [A | I] (Q = P [A | I]), per group
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int c = c0 + k, piv = __builtin_amdgcn_readfirstlane(pv[k]);
+            const int c = c0 + k;
             __builtin_amdgcn_wave_barrier();
-            if (piv != c) {
-                for (int cc = lane; cc < 2 * BS; cc += 64) {
-                    const double a = T[c * S + cc], bb = T[piv * S + cc];
-                    T[c * S + cc] = bb;
-                    T[piv * S + cc] = a;
+            if (gl && pv[k] != c) {
+                for (int cc = r; cc < 2 * BS; cc += BS) {
+                    const double x0 = Tg[c * S + cc], x1 = Tg[pv[k] * S + cc];
+                    Tg[c * S + cc] = x1;
+                    Tg[pv[k] * S + cc] = x0;
                 }
             }
         }
         __builtin_amdgcn_wave_barrier();
-        // Q += U Q[C, :]: the pivot rows (B operands) read before any tile is written
-        double bq[CT], ua[RT];
+        // Q += U Q[C, :] for every block: the pivot rows (B operands) read before any tile is written
+        double bq[NB][CT], ua[NB][RT];
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) bq[ct] = T[(c0 + (lane >> 4)) * S + ct * 16 + (lane & 15)];
+        for (int g = 0; g < NB; ++g) {
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) ua[rt] = W[(rt * 16 + (lane & 15)) * 4 + (lane >> 4)];
+            for (int ct = 0; ct < CT; ++ct) bq[g][ct] = Ts[wv][g][(c0 + (lane >> 4)) * S + ct * 16 + (lane & 15)];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) ua[g][rt] = Ws[wv][g][(rt * 16 + (lane & 15)) * 4 + (lane >> 4)];
+        }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
+        for (int g = 0; g < NB; ++g) {
+            double *T = Ts[wv][g];
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                d4v acc;
+            for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[i] = T[(rt * 16 + (lane >> 4) + 4 * i) * S + ct * 16 + (lane & 15)];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua[rt], bq[ct], acc, 0, 0, 0);
-                const int col = ct * 16 + (lane & 15);
+                for (int ct = 0; ct < CT; ++ct) {
+                    d4v acc;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = rt * 16 + (lane >> 4) + 4 * i;
-                    // the panel columns are exactly e_C after their eliminations
-                    T[r * S + col] = (col >= c0 && col < c0 + 4) ? (r == col ? 1.0 : 0.0) : acc[i];
+                    for (int i = 0; i < 4; ++i) acc[i] = T[(rt * 16 + (lane >> 4) + 4 * i) * S + ct * 16 + (lane & 15)];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua[g][rt], bq[g][ct], acc, 0, 0, 0);
+                    const int col = ct * 16 + (lane & 15);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int rr = rt * 16 + (lane >> 4) + 4 * i;
+                        // the panel columns are exactly e_C after their eliminations
+                        T[rr * S + col] = (col >= c0 && col < c0 + 4) ? (rr == col ? 1.0 : 0.0) : acc[i];
+                    }
                 }
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (sing && lane == 0) atomicMin(singular, (int)blk);
-    double *o = inv + (size_t)blk * BS * BS;
-    for (int e = lane; e < BS * BS; e += 64) o[e] = T[(e / BS) * S + BS + e % BS];
+    if (sing && r == 0) atomicMin(singular, (int)blk);
+    if (live) {
+        double *o = inv + (size_t)blk * BS * BS;
+        for (int e = r; e < BS * BS; e += BS) o[e] = Tg[(e / BS) * S + BS + e % BS];
+    }
 }
 
 template <typename VT>
@@ -2070,9 +2090,13 @@ static hipError_t bj_setup_mfma_t(const int32_t *indptr, const int32_t *indices,
                                   double *inv, int *sing, hipStream_t s) {
     const int64_t nb = (n + bs - 1) / bs;
     if (nb == 0) return hipSuccess;
-    const dim3 g((unsigned)((nb + 3) / 4));
-    if (bs == 16) hipLaunchKernelGGL((k_bj_setup_mfma<VT, 16>), g, dim3(256), 0, s, indptr, indices, data, n, nb, inv, sing);
-    else if (bs == 32) hipLaunchKernelGGL((k_bj_setup_mfma<VT, 32>), g, dim3(256), 0, s, indptr, indices, data, n, nb, inv, sing);
+    if (bs == 16) {   // 4 blocks per wave, 16 per workgroup
+        const dim3 g((unsigned)((nb + 15) / 16));
+        hipLaunchKernelGGL((k_bj_setup_mfma<VT, 16, 4>), g, dim3(256), 0, s, indptr, indices, data, n, nb, inv, sing);
+    } else if (bs == 32) {
+        const dim3 g((unsigned)((nb + 3) / 4));
+        hipLaunchKernelGGL((k_bj_setup_mfma<VT, 32, 1>), g, dim3(256), 0, s, indptr, indices, data, n, nb, inv, sing);
+    }
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
