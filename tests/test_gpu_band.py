@@ -141,3 +141,25 @@ def test_band_c1_vs_scipy_summary(vk_lib, gpu, golden_large):
     assert np.linalg.norm(x) == pytest.approx(g["x_norm2"], rel=1e-9)
     M.close()
     A.close()
+
+
+@pytest.mark.parametrize("shape", [(48, 8), (40, 816), (24, 1000)])
+def test_band_other_line_lengths(vk_lib, gpu, shape):
+    """Line lengths giving one part (L = 8), three parts of 272 rows (L = 816) and five parts of
+    200 rows (L = 1000): the v-halo rows between parts and the per-line boundary copies."""
+    p = twin.Vlasov(2, shape)
+    A = vk_lib.vlasov_operator(vk_lib.vlasov_params(2, shape), ctx=gpu)
+    assert A.line_band == shape[1]
+    M = vk_lib.block_jacobi(A, 8)
+    ip, ix, d = A.download()
+    b = coracle.rhs(p.n)
+    xb, ib, sb = _solve(vk_lib, gpu, A, M, b, True, maxiter=400)
+    xu, iu, su = _solve(vk_lib, gpu, A, M, b, False, maxiter=400)
+    assert sb.band == 1 and su.band == 0 and ib == iu == 0
+    assert abs(sb.inner_iters - su.inner_iters) <= 1
+    assert np.linalg.norm(xb - xu) / np.linalg.norm(xu) < 1e-9
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8, maxiter=400)
+    assert abs(sb.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(xb - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    M.close()
+    A.close()

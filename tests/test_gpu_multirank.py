@@ -65,7 +65,7 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
                                                        ("S2", 3, True, "dcgs2"), ("S4", 2, "npz", "dcgs2"),
                                                        ("C1", 2, False, "mgs"),
                                                        ("C1", 2, False, "dcgs2"), ("C1", 3, False, "dcgs2"),
-                                                       ("S2", 2, True, "dcgs2")])
+                                                       ("S2", 2, True, "dcgs2"), ("S2", 4, False, "dcgs2")])
 def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 

@@ -956,7 +956,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     // line-band DCGS2 step: one rank, SELL of uniform width 5 with coded columns (no wide chunk),
     // f64 values, tridiagonal BJ(8) (the fused step's TRIM apply), restart <= 20
     static const bool band_env = [] { const char *e = std::getenv("VTK_BAND"); return !(e && e[0] == '0'); }();
-    s.band = dc && band_env && c->band && A->band_L > 0 && A->band_L <= 800 && A->band_L % 8 == 0 &&
+    s.band = dc && band_env && c->band && A->band_L > 0 && A->band_L % 8 == 0 &&
              (!c->dist || !A->band_ghost || c->comm || c->host_comm) &&
              A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
              M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_fused(M) && bj_op(M).tri != nullptr && m >= 2 && m <= 20;

@@ -16,6 +16,7 @@ raises.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 from dataclasses import dataclass
 
@@ -30,6 +31,11 @@ __all__ = ["Context", "default_context", "csr_matrix", "load_npz", "save_npz", "
            "vlasov_line_stride"]
 
 VlasovParams = _abi.VlasovParams
+
+# At interpreter exit the finalizers below may run in any order (a context before the operators
+# that use it); the process is ending, so they leave the native objects to the runtime.
+_exiting = [False]
+atexit.register(lambda: _exiting.__setitem__(0, True))
 
 
 def vlasov_params(dim: int, shape, *, fp32=False, vmax=6.0, E0=0.5, nu=0.05, alpha=0.25,
@@ -157,6 +163,8 @@ class Context:
             self._h = None
 
     def __del__(self):
+        if _exiting[0]:
+            return
         try:
             self.close()
         except Exception:
@@ -261,6 +269,8 @@ class CsrOperator:
             self._h = None
 
     def __del__(self):
+        if _exiting[0]:
+            return
         try:
             self.close()
         except Exception:
@@ -432,6 +442,8 @@ class BlockJacobi:
             self._h = None
 
     def __del__(self):
+        if _exiting[0]:
+            return
         try:
             self.close()
         except Exception:
@@ -509,6 +521,8 @@ class LineJacobi:
             self._h = None
 
     def __del__(self):
+        if _exiting[0]:
+            return
         try:
             self.close()
         except Exception:
