@@ -31,10 +31,11 @@ CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv
     "band_step": r"void vtk::k_band_step<",
     "spmv_bj_dc": r"void vtk::k_sell<(double|float), false, 4, 8, true,",
     "spmv": r"void vtk::k_sell<(double|float), false, 0, 1, false,",
+    "spmv_bj": r"void vtk::k_sell<(double|float), false, 2, 8, true,",
     "spmv_resid_bj": r"void vtk::k_sell<(double|float), false, 3, 8, true,",
     "spmv_csr": r"void vtk::k_spmv<(double|float), false, 0, 1",
     "spmv_bj_dc_csr": r"void vtk::k_spmv<(double|float), false, 4, 8",
-    "dc_dots": "void vtk::k_dc_dots_rows<",
+    "dc_dots": r"void vtk::k_dc_dots(_rows<\d+>)?\(",
     "line_dc": r"void vtk::k_line_apply<\d+, (true|false), true>",
     "line_apply": r"void vtk::k_line_apply<\d+, (true|false)(, false)?>",
     "dc_update": "void vtk::k_dc_update<",

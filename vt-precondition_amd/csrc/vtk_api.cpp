@@ -768,7 +768,11 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // every kernel of step j is tagged j: it returns at entry once stop_col < j
     // SpMV + BJ and the step's dots in one pass for BJ-fused tiles with bs <= 8 (larger blocks
     // would spill the fused kernel's registers)
-    const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8;
+    // ... except for rows wider than 8 (the 4D operator: 9 entries) without a halo to overlap:
+    // there the SpMV + BJ kernel and the streaming dots kernel beat the register-capped fused
+    // kernel (C4: 707 + 658 us vs 1473 us per step, 422 vs 405 it/s)
+    const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M);
+    const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9;
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
     const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
                          s.M->line.seg <= 32 && s.G <= GMAX;
