@@ -19,7 +19,9 @@ C-ABI as device pointers).
 
 Printed: ONE JSON line on rank 0 (the driver's contract), with `roofline` (the dominant
 kernel, timed live with HIP events on the context's stream) and `cpu_baseline` (SciPy, the
-north_star's reference scipy.sparse path, on a bounded sample of the same workload).
+north_star's reference scipy.sparse path: one full solve of the same operator and RHS to the
+same tolerance on the box's host cores; --cpu-sample bounds it to the first --cpu-inner inner
+iterations instead).
 """
 from __future__ import annotations
 
@@ -529,10 +531,18 @@ def main():
         dist.destroy_process_group()
 
 
+KERNEL_SOURCES = ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp")
+
+
 def kernels_sha16():
+    """SHA-256 (16 hex digits) of the device sources, in a fixed order (tools/pmc_summary.py
+    stamps its summaries with the same hash)."""
     import hashlib
-    with open(os.path.join(ROOT, "vt-precondition_amd", "csrc", "vtk_kernels.hip"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "vt-precondition_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def pmc_traffic(cls, config, world):

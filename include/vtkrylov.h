@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTK_ABI_VERSION 2
+#define VTK_ABI_VERSION 3
 
 typedef struct vtk_ctx vtk_ctx;
 typedef struct vtk_csr vtk_csr;
@@ -140,6 +140,20 @@ int vtk_halo_plan(int64_t n_global, const int64_t *offsets, int world, int rank,
                   int64_t nnz, const int32_t *indices, int32_t *local_indices,
                   int64_t *n_halo, int64_t *halo_cols, int64_t *halo_count_per_rank);
 
+/* Geometry of the line-band DCGS2 step (vtk_csr_set_line_band) for a slab of
+ * n_local rows in lines of line_len rows on a device with n_cu compute units (n_cu <= 0: 256).
+ * VTK_ERR_ARG when the step cannot run on such a slab: line_len not a multiple of 8, n_local
+ * not whole lines, fewer than 2 lines, or a slab (with its two halo lines) beyond the kernels'
+ * 32-bit row / column indices.  (ABI 3) */
+typedef struct {
+    int parts;          /* wavefronts per line, <= 56 rows each (> 1 needs couplings within v-1..v+1) */
+    int wg_per_range;   /* workgroups per line range */
+    int waves_per_wg;   /* wavefronts per workgroup (<= 8: two per SIMD) */
+    int ranges;         /* line ranges of one launch; every range walks its lines in order */
+    int64_t lines;      /* lines of the slab */
+} vtk_band_geometry;
+int vtk_line_band_plan(int64_t n_local, int64_t line_len, int n_cu, vtk_band_geometry *out);
+
 /* ---- device context / communicator ---------------------------------------------------- */
 int vtk_device_count(int *count);
 int vtk_ctx_create(int hip_device, vtk_ctx **out);      /* owns one hipStream_t */
@@ -189,11 +203,15 @@ int vtk_csr_get_layout(vtk_csr *A, int *layout_in_use);
 int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out);
 /* Line-band structure: rows form x-lines of `line_len` consecutive rows and
  * every column lies in the lines x-1, x, x+1 (mod n / line_len) of its row's line x -- the 2D
- * Vlasov operators with line_len = Nv (set automatically by vtk_csr_create_vlasov on one rank).
- * Checked on the device (VTK_ERR_ARG when the structure does not hold; line_len 0 clears it).
- * With it, vtk_gmres runs each DCGS2 update pass together with the next step's SpMV + BJ +
- * dots in one sweep (SELL layout, tridiagonal BJ(8), restart <= 20, one rank): the basis is
- * read once per Arnoldi step instead of twice.  Same operator, same update arithmetic. */
+ * Vlasov operators with line_len = Nv (set automatically by vtk_csr_create_vlasov, on one rank
+ * or across ranks).  Checked on the device (VTK_ERR_ARG when the structure does not hold;
+ * line_len 0 clears it; the local row count and its halo must fit 32-bit indices).  Across
+ * ranks (world > 1) the call is collective: each rank's slab must hold whole lines with the two
+ * neighbour lines as its halo, and the band is set on every rank or on none.  With it,
+ * vtk_gmres runs each DCGS2 update pass together with the next step's SpMV + BJ + dots in one
+ * sweep (SELL layout, tridiagonal BJ(8), restart <= 20; across ranks the neighbours' edge lines
+ * travel as ghost lines each step): the basis is read once per Arnoldi step instead of twice.
+ * Same operator, same update arithmetic. */
 int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len);
 int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len);
 

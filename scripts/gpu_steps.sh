@@ -70,6 +70,8 @@ for s in "$@"; do
                step slab_c3_1 300 python bench.py --config C3 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
                step slab_c4_8 300 python bench.py --config C4 --slab 8 --comm-solo --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
         benchc2full) step benchc2full 600 python bench.py --config C2 ;;
+        abband) for rep in 1 2; do for impl in wave wg; do VTK_PROF_PERJ=1 VTK_BAND_IMPL=$impl step abband_${impl}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 ${BENCH_ARGS:-} || exit $?; python tools/band_perj.py gpurun_out/abband_${impl}_$rep.log; done; done ;;
+        testsv) step testsv 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         large) step large 600 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

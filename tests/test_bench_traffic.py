@@ -1,5 +1,5 @@
 """bench.py's roofline.traffic gate (CPU): PMC HBM bytes are reported only from a committed
-profiles/rNN[_tag]_pmc_traffic.json of the same config AND the same vtk_kernels.hip source
+profiles/rNN[_tag]_pmc_traffic.json of the same config AND the same device sources (bench.KERNEL_SOURCES)
 (a summary of other kernels must never be reported as this run's traffic)."""
 import hashlib
 import json
@@ -11,9 +11,13 @@ import bench
 def _tree(tmp_path, src=b"// kernels v1\n"):
     d = tmp_path / "vt-precondition_amd" / "csrc"
     d.mkdir(parents=True)
-    (d / "vtk_kernels.hip").write_bytes(src)
+    h = hashlib.sha256()
+    for i, name in enumerate(bench.KERNEL_SOURCES):   # every device source is hashed, in order
+        body = src + bytes(f"// {i}\n", "ascii")
+        (d / name).write_bytes(body)
+        h.update(body)
     (tmp_path / "profiles").mkdir()
-    return hashlib.sha256(src).hexdigest()[:16]
+    return h.hexdigest()[:16]
 
 
 def _summary(tmp_path, name, config, sha, bytes_per_launch):

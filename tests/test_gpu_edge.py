@@ -84,3 +84,28 @@ def test_device_csr_input(gpu, vk_lib):
                           shape=(n, n), ctx=gpu)
         with pytest.raises(ValueError, match="column index out of range"):
             vk.csr_matrix((d, ixb, ip), shape=(n, n), ctx=gpu)
+
+
+def test_device_csr_spare_capacity_and_stream(gpu, vk_lib):
+    """Device CSR whose indices / data carry spare capacity past indptr[-1]: nnz is
+    taken from indptr, the spare entries are ignored; the conversions run on a non-default torch
+    stream and are complete before the library copies them."""
+    import torch
+    vk = vk_lib
+    n = 257
+    ip, ix, d = tridiag(n)
+    dev = torch.device("cuda", 0)
+    spare = 37
+    ixs = np.concatenate([ix, np.full(spare, 1 << 30, np.int32)])   # garbage beyond nnz
+    ds = np.concatenate([d, np.full(spare, np.nan)])
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        td = torch.from_numpy(ds).to(dev, non_blocking=True).to(torch.float32).to(torch.float64)
+        tix = torch.from_numpy(ixs.astype(np.int64)).to(dev)
+        tip = torch.from_numpy(ip.astype(np.int64)).to(dev)
+        A = vk.csr_matrix((td, tix, tip), shape=(n, n), ctx=gpu)
+    x = twin.rhs(n, seed=0xC0FFEE)
+    d32 = d.astype(np.float32).astype(np.float64)
+    assert np.array_equal(A @ x, coracle.spmv(ip, ix, d32, x))
+    with pytest.raises(TypeError):
+        vk.csr_matrix((td, tix, tip.to("cpu")), shape=(n, n), ctx=gpu)

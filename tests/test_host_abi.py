@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(vk_lib):
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(vk_lib._abi.PROTOTYPES), set(names) ^ set(vk_lib._abi.PROTOTYPES)
-    assert vk_lib._abi.lib().vtk_abi_version() == 2
+    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 3
 
 
 def test_status_strings(vk_lib):
@@ -160,3 +160,32 @@ def test_host_code_under_asan_ubsan():
     r = subprocess.run(["bash", os.path.join(root, "tools", "asan_host.sh")], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0 and "asan_host: ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def _band_plan(vk_lib, n, L, ncu=256):
+    import ctypes
+    g = vk_lib._abi.BandGeometry()
+    st = vk_lib._abi.lib().vtk_line_band_plan(n, L, ncu, ctypes.byref(g))
+    return st, g
+
+
+def test_line_band_plan_geometry(vk_lib):
+    """The band step's geometry (vtk_line_band_plan, ABI 3): C3 = 25 000 lines of 800 rows ->
+    15 parts of <= 56 rows in two 8-wave workgroups per range, one workgroup per CU."""
+    st, g = _band_plan(vk_lib, 20_000_000, 800)
+    assert st == vk_lib._abi.OK
+    assert (g.parts, g.wg_per_range, g.waves_per_wg, g.ranges, g.lines) == (15, 2, 8, 128, 25_000)
+    st, g = _band_plan(vk_lib, 64 * 32, 32)   # S2: one part per line, one-wave workgroups
+    assert st == vk_lib._abi.OK and (g.parts, g.wg_per_range, g.waves_per_wg, g.ranges) == (1, 1, 1, 32)
+    st, g = _band_plan(vk_lib, 24 * 1000, 1000)   # 125 blocks: 18 parts, 3 workgroups of 6 waves
+    assert st == vk_lib._abi.OK and g.parts == 18 and g.wg_per_range * g.waves_per_wg >= 18 and g.waves_per_wg <= 8
+    assert g.ranges == 12   # X / 2
+
+
+@pytest.mark.parametrize("n,L", [(2**31, 1024), (2**30 + 2**20, 1024), (800 * 7 + 8, 800), (800, 800), (1000, 100), (0, 8)])
+def test_line_band_plan_rejects(vk_lib, n, L):
+    """32-bit index guard (slabs whose rows + halo reach 2^30), partial lines, one line, line
+    lengths not a multiple of 8: VTK_ERR_ARG with a message, no GPU needed."""
+    st, _ = _band_plan(vk_lib, n, L)
+    assert st == vk_lib._abi.ERR_ARG
+    assert vk_lib._abi.last_error()

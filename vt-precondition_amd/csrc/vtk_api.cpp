@@ -284,7 +284,9 @@ Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
 
 int halo_exchange(vtk_csr *A, const double *x) {
     vtk_ctx *c = A->ctx;
-    if (!c->dist || (A->n_send == 0 && A->n_halo == 0)) return VTK_OK;   // no peer of this rank
+    // no peer of this rank: RCCL point-to-point needs no call; the host-staged alltoallv is a
+    // collective every rank joins (with zero counts)
+    if (!c->dist || (!c->host_comm && A->n_send == 0 && A->n_halo == 0)) return VTK_OK;
     Prof pf(c, "halo", -1, 16.0 * A->n_send + 8.0 * A->n_halo);
     HIPCHK(c, launch_gather(x, A->d_send_idx, A->n_send, A->d_send_buf, c->stream));
     return comm_alltoallv(c, A->d_send_buf, A->send_cnt, A->send_off, A->d_halo, A->recv_cnt, A->recv_off, ncclDouble, sizeof(double));
@@ -619,8 +621,16 @@ void destroy_csr(vtk_csr *A) {
 // in the lines x-1..x+1 (mod X) of the row's line; VTK_ERR_ARG (no error text) otherwise
 // Distributed operators (world > 1, or a one-rank communicator): the slab must hold whole lines
 // and its halo must be exactly the two neighbour lines (left: the line before the slab, right: the
-// one after it, periodic); the per-step ghost exchange layout is derived here.
-int band_check_dist(vtk_csr *A, int64_t L, bool &solo) {
+// one after it, periodic); the per-step ghost exchange layout is derived here
+// into `out`, which the caller commits only once the whole check has passed.
+struct BandLayout {
+    int lblk = 0;
+    int peer[2] = {-1, -1};
+    std::vector<int64_t> scnt, soff, rcnt, roff;
+    int64_t off_first = -1, off_last = -1, off_left = -1, off_right = -1;
+};
+
+int band_check_dist(vtk_csr *A, int64_t L, bool &solo, BandLayout &out) {
     vtk_ctx *c = A->ctx;
     const int64_t n = A->n_local, Xg = A->n_global / L;
     solo = A->n_halo == 0 && A->n_send == 0;
@@ -635,7 +645,7 @@ int band_check_dist(vtk_csr *A, int64_t L, bool &solo) {
             if (A->halo_cols[(size_t)(b * L + v)] != gl[b] * L + v) return VTK_ERR_ARG;
     }
     if (!((gl[0] == left && gl[1] == right) || (gl[0] == right && gl[1] == left))) return VTK_ERR_ARG;
-    A->band_lblk = gl[0] == left ? 0 : 1;
+    out.lblk = gl[0] == left ? 0 : 1;
     auto owner = [&](int64_t line) {
         for (int q = 0; q < c->world; ++q)
             if (A->offsets[q] <= line * L && line * L < A->offsets[q + 1]) return q;
@@ -643,49 +653,90 @@ int band_check_dist(vtk_csr *A, int64_t L, bool &solo) {
     };
     const int pl = owner(left), pr = owner(right);
     if (pl < 0 || pr < 0 || pl == c->rank || pr == c->rank) return VTK_ERR_ARG;
-    A->band_peer[0] = pl;
-    A->band_peer[1] = pr;
+    out.peer[0] = pl;
+    out.peer[1] = pr;
     // per peer: sends [my last line if it is my right neighbour][my first line if it is my left],
     // receives [into the left ghost if it is my left neighbour][into the right ghost if my right]:
     // a pair that is both (two ranks) matches last line -> left ghost, first line -> right ghost
     const int W = c->world;
-    A->band_scnt.assign(W, 0);
-    A->band_soff.assign(W, 0);
-    A->band_rcnt.assign(W, 0);
-    A->band_roff.assign(W, 0);
+    out.scnt.assign(W, 0);
+    out.soff.assign(W, 0);
+    out.rcnt.assign(W, 0);
+    out.roff.assign(W, 0);
     int64_t so = 0, ro = 0;
     for (int q = 0; q < W; ++q) {
-        A->band_soff[q] = so;
-        A->band_roff[q] = ro;
-        if (q == pr) { A->band_off_last = so; so += 3 * L; }
-        if (q == pl) { A->band_off_first = so; so += 3 * L; }
-        if (q == pl) { A->band_off_left = ro; ro += 3 * L; }
-        if (q == pr) { A->band_off_right = ro; ro += 3 * L; }
-        A->band_scnt[q] = so - A->band_soff[q];
-        A->band_rcnt[q] = ro - A->band_roff[q];
+        out.soff[q] = so;
+        out.roff[q] = ro;
+        if (q == pr) { out.off_last = so; so += 3 * L; }
+        if (q == pl) { out.off_first = so; so += 3 * L; }
+        if (q == pl) { out.off_left = ro; ro += 3 * L; }
+        if (q == pr) { out.off_right = ro; ro += 3 * L; }
+        out.scnt[q] = so - out.soff[q];
+        out.rcnt[q] = ro - out.roff[q];
     }
     return VTK_OK;
 }
 
-int band_check(vtk_csr *A, int64_t L) {
+// local check of line length L (no collective): on success `out` holds the layout and the
+// v-locality / ghost flags for band_check_all to commit
+struct BandCheck {
+    BandLayout lay;
+    bool vloc = false, ghost = false;
+};
+
+int band_check(vtk_csr *A, int64_t L, BandCheck &out) {
     vtk_ctx *c = A->ctx;
     const int64_t n = A->n_local;
-    if (L <= 0 || n % L != 0 || n / L < 2 || n / L > INT32_MAX || L > INT32_MAX || n + 2 * L >= INT32_MAX)
-        return VTK_ERR_ARG;
+    // whole lines, >= 2 of them, rows and halo columns within the kernels' 32-bit indices
+    vtk_band_geometry geo{};
+    if (vtk_line_band_plan(n, L, c->n_cu, &geo) != VTK_OK) return VTK_ERR_ARG;
     bool solo = true;
-    if (c->dist && band_check_dist(A, L, solo) != VTK_OK) return VTK_ERR_ARG;
+    if (c->dist && band_check_dist(A, L, solo, out.lay) != VTK_OK) return VTK_ERR_ARG;
     if (solo && n / L < 3) return VTK_ERR_ARG;
     DBuf bad;
     TRY(dalloc(c, bad, sizeof(int)));
     HIPCHK(c, hipMemsetAsync(bad.p, 0, sizeof(int), c->stream));
     if (solo) HIPCHK(c, launch_band_check(A->d_indptr, A->d_indices, n, (int)L, (int)(n / L), bad.as<int>(), c->stream));
-    else HIPCHK(c, launch_band_check_dist(A->d_indptr, A->d_indices, n, (int)L, A->band_lblk, bad.as<int>(), c->stream));
+    else HIPCHK(c, launch_band_check_dist(A->d_indptr, A->d_indices, n, (int)L, out.lay.lblk, bad.as<int>(), c->stream));
     int hb = 1;
     HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (hb & 1) return VTK_ERR_ARG;
-    A->band_vloc = (hb & 2) == 0;
-    A->band_ghost = !solo;
+    out.vloc = (hb & 2) == 0;
+    out.ghost = !solo;
+    return VTK_OK;
+}
+
+// band_check on every rank, then one agreement: the line band is set on all ranks or on none
+// (collective when the context is distributed).  VTK_OK: set; VTK_ERR_ARG: not a line-band
+// operator on some rank; other codes: a HIP / communicator failure on this rank.
+int band_check_all(vtk_csr *A, int64_t L) {
+    vtk_ctx *c = A->ctx;
+    BandCheck chk;
+    int rc = band_check(A, L, chk);
+    if (c->dist) {
+        double mine = rc == VTK_OK ? 0.0 : 1.0, bad = 0.0;
+        HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        TRY(comm_allreduce(c, &c->d_scal[DC_NQ], 1));
+        HIPCHK(c, hipMemcpyAsync(&bad, &c->d_scal[DC_NQ], sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (rc == VTK_OK && bad != 0.0) rc = VTK_ERR_ARG;
+    }
+    if (rc != VTK_OK) return rc;
+    // every rank passed: commit the layout together with band_L (set by the caller)
+    A->band_vloc = chk.vloc;
+    A->band_ghost = chk.ghost;
+    A->band_lblk = chk.lay.lblk;
+    A->band_peer[0] = chk.lay.peer[0];
+    A->band_peer[1] = chk.lay.peer[1];
+    A->band_scnt = chk.lay.scnt;
+    A->band_soff = chk.lay.soff;
+    A->band_rcnt = chk.lay.rcnt;
+    A->band_roff = chk.lay.roff;
+    A->band_off_first = chk.lay.off_first;
+    A->band_off_last = chk.lay.off_last;
+    A->band_off_left = chk.lay.off_left;
+    A->band_off_right = chk.lay.off_right;
     return VTK_OK;
 }
 
@@ -712,7 +763,8 @@ struct Solver {
     // line-band DCGS2 step (k_band_step): grid, w double buffer (s.w / s.tmp by step parity),
     // first/last-line copies of p per workgroup (two sets, by step parity)
     bool band = false;
-    int band_G = 0, band_H = 1;
+    bool band_wave = true;                   // k_band_wave (default) or k_band_step (VTK_BAND_IMPL=wg)
+    int band_G = 0, band_H = 1, band_gp = 1, band_hw = 1;
     double *edge[2] = {nullptr, nullptr};
     double *vedge[2] = {nullptr, nullptr};   // per-line part-boundary rows of p (band_H > 1)
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
@@ -827,7 +879,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                 std::max<double>(1.0, (double)n);
             // a rank with no x-neighbour data to send or receive (one rank) skips the exchange
             // and its event hand-offs; one without boundary rows skips the boundary launch
-            const bool exch = s.A->n_send > 0 || s.A->n_halo > 0;
+            const bool exch = s.A->n_send > 0 || s.A->n_halo > 0 || c->host_comm;
             const bool has_bd = s.A->use_sell ? s.A->g_bd.count > 0 : s.M->tiles_bd.ntiles > 0;
             if (exch) TRY(halo_exchange_async(s.A, pj));
             {
@@ -883,7 +935,14 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         }
         if (band && j <= m - 2) {
             // update pass of step j + SpMV, BJ and dots of step j+1 in one sweep over the x-lines
-            Prof pf(c, "band_step", j, b_csr + b_inv + n8 * (j + 6));   // V_j, p_j, w_j, v_j, p_j+1, w_j+1
+            // reads V_k (k < j), p_j, w_j; writes v_j (j >= 1: p_j is v_0 at j = 0), p_{j+1}, w_{j+1}
+            // (VTK_PROF_PERJ=1: one profile class per step index, "band_step_jNN")
+            static const bool perj = [] { const char *e = std::getenv("VTK_PROF_PERJ"); return e && e[0] == '1'; }();
+            static const char *const jname[] = {"band_step_j00", "band_step_j01", "band_step_j02", "band_step_j03",
+                "band_step_j04", "band_step_j05", "band_step_j06", "band_step_j07", "band_step_j08", "band_step_j09",
+                "band_step_j10", "band_step_j11", "band_step_j12", "band_step_j13", "band_step_j14", "band_step_j15",
+                "band_step_j16", "band_step_j17", "band_step_j18", "band_step_j19"};
+            Prof pf(c, perj && j < 20 ? jname[j] : "band_step", j, b_csr + b_inv + n8 * (j + (j >= 1 ? 5 : 4)));
             BandK a;
             a.pk = s.A->sell.d_pk;
             a.dict = s.A->sell.d_dict;
@@ -911,8 +970,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.H_parts = s.band_H;
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
-            a.lmagic = (uint64_t)((((uint64_t)1 << 40) + (uint64_t)s.A->band_L - 1) / (uint64_t)s.A->band_L);
-            HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
+            a.gp = s.band_gp;
+            if (s.band_wave) HIPCHK(c, launch_band_wave(a, s.band_G, s.band_hw, s.A->sell.uniform_w, c->stream));
+            else HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
             HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
@@ -965,18 +1025,51 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
              A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
              M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_fused(M) && bj_op(M).tri != nullptr && m >= 2 && m <= 20;
     int band_R = 0;
+    static const bool band_wave_env = [] { const char *e = std::getenv("VTK_BAND_IMPL"); return !(e && std::strcmp(e, "wg") == 0); }();
+    s.band_wave = band_wave_env;
     if (s.band) {
-        // parts per line (rows per workgroup <= 400; > 1 needs the v-locality of the couplings),
-        // two workgroups per CU, >= 2 lines per range
         const int64_t X = n / A->band_L;
-        s.band_H = band_parts(A->band_L);
-        if (s.band_H < 1 || (s.band_H > 1 && !A->band_vloc)) s.band = false;
-        else {
-            const int64_t wg = (int64_t)band_wg_per_cu() * (c->n_cu > 0 ? c->n_cu : 256);
-            band_R = (int)std::min<int64_t>({wg / s.band_H, X / 2, (int64_t)GMAX / s.band_H});
-            s.band_G = band_R * s.band_H;
-            if (band_R < 1) s.band = false;
+        const int64_t ncu = c->n_cu > 0 ? c->n_cu : 256;
+        if (s.band_wave) {
+            // wave-independent step: parts of <= 56 rows (> 1 part needs the v-locality of the
+            // couplings), gp workgroups of <= 8 waves per line range, as many workgroups as fit
+            // at 2 waves/SIMD (8 waves per CU: L = 800 -> 128 ranges of two workgroups), >= 2
+            // lines per range.  The geometry is the same for every step of the cycle (the edge
+            // copies one step writes are indexed by the ranges of the next).
+            vtk_band_geometry g{};
+            if (vtk_line_band_plan(n, A->band_L, (int)ncu, &g) != VTK_OK || (g.parts > 1 && !A->band_vloc)) {
+                s.band = false;
+            } else {
+                band_R = g.ranges;
+                s.band_H = g.parts;
+                s.band_gp = g.wg_per_range;
+                s.band_hw = g.waves_per_wg;
+                s.band_G = band_R * g.wg_per_range;
+                if (band_R < 1) s.band = false;
+            }
+        } else {
+            // round-2 workgroup step: parts per line (rows per workgroup <= 400; > 1 needs the
+            // v-locality of the couplings), two workgroups per CU, >= 2 lines per range
+            s.band_H = band_parts(A->band_L);
+            if (s.band_H < 1 || (s.band_H > 1 && !A->band_vloc)) s.band = false;
+            else {
+                const int64_t wg = (int64_t)band_wg_per_cu() * ncu;
+                band_R = (int)std::min<int64_t>({wg / s.band_H, X / 2, (int64_t)GMAX / s.band_H});
+                s.band_G = band_R * s.band_H;
+                if (band_R < 1) s.band = false;
+            }
         }
+    }
+    // every rank takes the same path: the band step exchanges ghost lines with its neighbours
+    // each step, so one rank falling back alone would leave its peers' sends unmatched
+    if (c->dist) {
+        double mine = s.band ? 0.0 : 1.0;
+        HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        TRY(comm_allreduce(c, &c->d_scal[DC_NQ], 1));
+        double off = 0.0;
+        HIPCHK(c, hipMemcpyAsync(&off, &c->d_scal[DC_NQ], sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (off != 0.0) s.band = false;
     }
     const size_t nedge1 = s.band ? (size_t)band_R * 2 * A->band_L : 0;
     const size_t nvedge1 = s.band ? (size_t)(n / A->band_L) * s.band_H * 2 : 0;
@@ -1446,7 +1539,11 @@ int vtk_csr_create_vlasov(vtk_ctx *c, const vtk_vlasov_params *p, const int64_t 
     HIPCHK(c, launch_vlasov_fill(*p, A->row_begin, nl, A->d_indptr, A->d_indices, A->d_data, c->stream));
     TRY(finish_csr(A));
     // the 2D operator's rows form x-lines of Nv rows coupled to the neighbouring lines only
-    if (p->dim == 2 && band_check(A, p->shape[1]) == VTK_OK) A->band_L = p->shape[1];
+    if (p->dim == 2) {
+        const int brc = band_check_all(A, p->shape[1]);
+        if (brc == VTK_OK) A->band_L = p->shape[1];
+        else if (brc != VTK_ERR_ARG) return brc;
+    }
     *out = A;
     A = nullptr;
     return VTK_OK;
@@ -1782,7 +1879,7 @@ int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len) {
         A->band_L = 0;
         return VTK_OK;
     }
-    const int rc = band_check(A, line_len);
+    const int rc = band_check_all(A, line_len);
     if (rc == VTK_ERR_ARG)
         return fail(c, VTK_ERR_ARG, "vtk_csr_set_line_band: not a line-band operator for this line length "
                                     "(line_len | n, >= 3 lines, every column in lines x-1..x+1; across ranks: "

@@ -1,0 +1,704 @@
+// vtk_band.hip — the line-band DCGS2 step and its ghost-line exchange and
+// structure checks, gfx950.  Built with -ffp-contract=off like vtk_kernels.hip: the update,
+// SpMV and block-Jacobi arithmetic is bit-identical to k_dc_update / k_sell.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "vtk_device.hpp"
+
+namespace vtk {
+
+// ------------------------------------------------------------------------------------------
+// Line-band DCGS2 step.  For an operator whose rows form x-lines of L rows
+// (row = x L + v) with every column in lines x-1, x, x+1 (periodic in x) at v-1..v+1 -- the 2D
+// Vlasov operators, L = Nv -- the update pass of step j and the fused SpMV + BJ + dots of step
+// j+1 run as ONE sweep.  Workgroup (range r, part h) owns rows v0 <= v < v0 + LP (LP = L / H)
+// of the lines [xa, xb) of range r and walks them in order; at line x it
+//   1. updates line x+1 (v_j, p_{j+1} exactly as k_dc_update) on its rows plus one v-halo row
+//      on each side, and puts p_{j+1}(x+1) into an LDS ring of 4 lines,
+//   2. computes w(x) = M^-1 A p_{j+1} on its rows of line x from the ring (the SELL entries in
+//      stored order and the tridiagonal BJ solve exactly as k_sell: w is bit-identical),
+//   3. accumulates step j+1's dots s = V_{j+1}^T p_{j+1}, z = V_{j+1}^T w, |p|^2, p.w, |w|^2
+//      from LDS: the line's basis rows were staged there by step 1 one line earlier.
+// The basis is read from HBM once per step instead of twice (update pass + dots), p_{j+1} is
+// never re-read for the SpMV gathers, and one launch replaces two.  Rows another workgroup owns
+// are recomputed: the x-halo lines xa-1 and xb (their p_j from the owner's copy of its first /
+// last line from the previous step -- the owner overwrites p_j in place with v_j) and the
+// v-halo rows v0-1, v0+LP (p_j from the owner's per-line boundary copies).  7 waves; lane
+// tid <-> row v = v0 - 8 + tid (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two
+// workgroups per CU, whose update / SpMV / dots phases overlap.
+// ------------------------------------------------------------------------------------------
+constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
+// geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
+// 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU)
+template <int GEO> struct BandGeo;
+template <> struct BandGeo<2> { static constexpr int LP = 400, T = 448, WPC = 2; };
+template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4; };
+#ifndef VTK_BAND_GEO
+#define VTK_BAND_GEO 2
+#endif
+#ifndef VTK_BAND_DOTS_UNROLL
+#define VTK_BAND_DOTS_UNROLL 2   // the dots' 64-row passes issued together (LDS latency once per group)
+#endif
+#ifndef VTK_BAND_REREAD
+#define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
+#endif
+#ifndef VTK_BAND_PF
+#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 8)   // j <= this: next line's update operands prefetched across SpMV + dots
+#endif
+#ifndef VTK_BAND_VBUF_FIXED
+#define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
+#endif
+
+template <int WU, int J, int GEO>
+__global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
+    constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
+    constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
+    __shared__ double vbuf[VTK_BAND_REREAD ? 1 : (VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
+    __shared__ double ring[4 * BAND_RS];
+    __shared__ double wbuf[BAND_LP];
+    __shared__ double red[DC_NQ];
+    __shared__ double cs[BAND_JV], ce[BAND_JV];
+    constexpr int j = J;
+    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
+        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m);
+        return;
+    }
+    if (stopped(&a.st->stop_col, j)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int L = a.L, X = a.X, H = a.H_parts, LP = L / H;
+    const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
+    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
+    const int v = v0 - 8 + tid;
+    const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
+    const bool own = tid >= 8 && tid < 8 + LP;
+    const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
+    const int ii = lane & 7;
+    for (int k = tid; k < j; k += BAND_T) {
+        cs[k] = a.cf->s[k];
+        ce[k] = a.cf->e[k];
+    }
+    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j];
+    __syncthreads();
+    double vreg[J + 1];
+    double acc[BAND_IT][3];
+#pragma unroll
+    for (int u = 0; u < BAND_IT; ++u) acc[u][0] = acc[u][1] = acc[u][2] = 0.0;
+    // update of line y on the lane's row: kind 0 an owned line, 1 / 2 the x-halo line before xa /
+    // after xb-1 (p_j from the owner's edge copy; nothing stored); owned lines' v-halo rows take
+    // p_j from the neighbour part's boundary copy.  vreg = V_k(y) k < j, then v_j.
+    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1)
+    const int nl = xb - xa;
+    auto line_of = [&](int it, int &kind) {
+        kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
+        return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
+    };
+    // update operands of iteration it's line on the lane's row: V_k (k < j), p_j, w_j.  kind 1 / 2
+    // (x-halo lines): p_j from the owner's edge copy; owned lines' v-halo rows: p_j from the
+    // neighbour part's boundary copy (the owners overwrite p_j in place with v_j)
+    struct Ld {
+        double v[J > 0 ? J : 1];
+        double pj, wj;
+    };
+    auto load = [&](int it, Ld &o) {
+        int kind;
+        const int y = line_of(it, kind);
+        const int64_t row = (int64_t)y * L + (upd ? v : 0);
+        o.pj = 0.0;
+        o.wj = 0.0;
+        // a rank's first / last line range: the x-halo line is a neighbour rank's line, whose
+        // V_k, p_j, w_j arrived in the ghost buffer (slots k, m, m + 1)
+        const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
+                               ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
+        if (upd) {
+            if (gh) {
+                o.pj = gh[(size_t)a.m * L + v];
+                o.wj = gh[(size_t)(a.m + 1) * L + v];
+            } else {
+                if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
+                else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
+                else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
+                else o.pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
+                o.wj = __builtin_nontemporal_load(a.w_in + row);
+            }
+        }
+        if (gh) {
+#pragma unroll
+            for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < J; ++k)
+                o.v[k] = upd ? (VTK_BAND_REREAD ? a.V[(size_t)k * a.ld + row]
+                                                : __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row)) : 0.0;
+        }
+    };
+    // the update itself (k_dc_update's operations); stores on owned lines; vreg = V_k, v_j
+    auto update = [&](int it, const Ld &o) -> double {
+        int kind;
+        const int y = line_of(it, kind);
+        const int64_t row = (int64_t)y * L + (upd ? v : 0);
+#pragma unroll
+        for (int k = 0; k < J; ++k) vreg[k] = o.v[k];
+        double av = o.pj, tv = o.wj;
+#pragma unroll
+        for (int k = 0; k < J; ++k) {
+            const double sk = cs[k], ek = ce[k];
+            av = av - sk * vreg[k];
+            tv = tv - ek * vreg[k];
+        }
+        double vj = o.pj;
+        if (j >= 1) vj = av * rinv;
+        tv = tv - ej * vj;
+        const double pn = tv * qc;
+        vreg[J] = vj;
+        if (kind == 0 && own) {
+            if (j >= 1) {
+                if constexpr (VTK_BAND_REREAD) a.V[(size_t)j * a.ld + row] = vj;
+                else __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+            }
+            __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
+            if (y == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
+            if (y == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
+            if (H > 1 && tid == 8) a.vedge_out[((size_t)y * H + h) * 2] = pn;
+            if (H > 1 && tid == 7 + LP) a.vedge_out[((size_t)y * H + h) * 2 + 1] = pn;
+        }
+        return pn;
+    };
+    auto stage = [&]() {
+        if (!VTK_BAND_REREAD && own) {
+#pragma unroll
+            for (int k = 0; k <= J; ++k) vbuf[k * BAND_LP + tid - 8] = vreg[k];
+        }
+    };
+    auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
+    // iteration it updates line y = xa - 1 + it and, from it = 2 on, runs the SpMV and dots of
+    // line y - 1.  PF (small j, registers allow): the next line's update operands are loaded
+    // during this line's SpMV and dots (software pipeline)
+    constexpr bool PF = J <= VTK_BAND_PF;
+    Ld nx;
+    if constexpr (PF) load(0, nx);
+    for (int it = 0; it <= nl + 1; ++it) {
+        const int y = xa - 1 + it, x = y - 1;
+        const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
+        const int64_t lrow = (int64_t)(work ? x : xa) * L;
+        const int64_t row = lrow + (own ? v : v0);
+        // the SpMV operands of line x (independent of the update): codes, dictionary, values, m
+        const int64_t q = row >> 6, q0 = (lrow + v0 - 8 + 64 * wv) >> 6;
+        const int l64 = (int)(row & 63);
+        uint32_t word = 0u;
+        int dv = 0;
+        double d[WU];
+        double mrow = 1.0;
+        if (work) {
+            word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
+            const int64_t qd = q0 + (lane >> 4);
+            dv = (lane < 32 && qd >= 0 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
+#pragma unroll
+            for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
+            if (own) mrow = __builtin_nontemporal_load(a.mtri + row);
+        }
+        // 1. update of line y
+        {
+            Ld cu;
+            if constexpr (PF) cu = nx;
+            else load(it, cu);
+            const double pn = update(it, cu);
+            if (upd) ring[slot(y) + tid] = pn;
+            if constexpr (PF) {
+                if (it <= nl) load(it + 1, nx);
+            }
+        }
+        __syncthreads();
+        if (work) {
+            // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
+            double sacc = 0.0, sub = 0.0, sup = 0.0;
+            const int sel = (int)(q - q0) * 16;
+#pragma unroll
+            for (int k = 0; k < WU; ++k) {
+                const int code = (int)((word >> (4 * k)) & 15u);
+                const int off = __shfl(dv, (sel + code) & 63, 64);
+                if (own && code != PK_CODES) {
+                    // the column's line relative to x and its position in that line, by range
+                    // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
+                    const int t = v + off;
+                    int rel, vc;
+                    const int c = x * L + t;
+                    if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
+                        const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
+                        rel = blk == a.left_blk ? -1 : 1;
+                        vc = kk - blk * L;
+                    } else if (t >= 0 && t < L) { rel = 0; vc = t; }
+                    else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
+                    else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
+                    else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
+                    else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
+                    const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
+                    sacc += d[k] * xv;
+                    if (off == -1 && ii > 0) sub = sub + d[k];
+                    if (off == 1 && ii < 7) sup = sup + d[k];
+                }
+            }
+            const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
+            if (own) {
+                __builtin_nontemporal_store(z, a.w_out + row);
+                wbuf[tid - 8] = z;
+            }
+            __syncthreads();
+            // 3. dots of the part's rows of line x: wave wv owns items wv, wv + 7, wv + 14 (item
+            //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows
+            const double *pr = ring + slot(x) + 8;
+#pragma unroll
+            for (int u = 0; u < BAND_IT; ++u) {
+                const int itm = wv + BAND_W * u;
+                if (itm <= j) {
+                    const double *vk = VTK_BAND_REREAD ? a.V + (size_t)itm * a.ld + (int64_t)x * L + v0
+                                                       : vbuf + itm * BAND_LP;
+#pragma unroll VTK_BAND_DOTS_UNROLL
+                    for (int t = lane; t < LP; t += 64) {
+                        const double vv = vk[t];
+                        acc[u][0] += vv * pr[t];
+                        acc[u][1] += vv * wbuf[t];
+                    }
+                } else if (itm == j + 1) {
+#pragma unroll VTK_BAND_DOTS_UNROLL
+                    for (int t = lane; t < LP; t += 64) {
+                        const double pv = pr[t], wq = wbuf[t];
+                        acc[u][0] += pv * pv;
+                        acc[u][1] += pv * wq;
+                        acc[u][2] += wq * wq;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (it >= 1 && it <= nl) stage();   // line y is owned: its basis rows for the dots one line on
+    }
+    // per-workgroup partials in launch_dc_dots' layout for step j+1
+#pragma unroll
+    for (int u = 0; u < BAND_IT; ++u) {
+        const int itm = wv + BAND_W * u;
+        if (itm <= j + 1) {   // wave-uniform
+            const double t0 = wave_allsum(acc[u][0]), t1 = wave_allsum(acc[u][1]), t2 = wave_allsum(acc[u][2]);
+            if (lane == 0) {
+                if (itm <= j) {
+                    red[itm] = t0;
+                    red[DC_MAXJ + itm] = t1;
+                } else {
+                    red[2 * DC_MAXJ] = t0;
+                    red[2 * DC_MAXJ + 1] = t1;
+                    red[2 * DC_MAXJ + 2] = t2;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int jn = j + 1;
+    for (int qq = tid; qq < DC_NQ; qq += BAND_T) {
+        const bool used = qq < jn || (qq >= DC_MAXJ && qq < DC_MAXJ + jn) || qq >= 2 * DC_MAXJ;
+        if (used) a.part[(size_t)qq * GMAX + b] = red[qq];
+    }
+}
+
+int band_wg_per_cu() { return BandGeo<VTK_BAND_GEO>::WPC; }
+int band_parts(int64_t L) {
+    const int lp = BandGeo<VTK_BAND_GEO>::LP;
+    for (int h = 1; h <= 16; ++h)
+        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= lp) return h;
+    return 0;
+}
+
+hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
+    constexpr int lp = BandGeo<VTK_BAND_GEO>::LP;
+    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > lp || (a.L / a.H_parts) % 8 != 0 ||
+        a.j + 1 > BAND_JV || grid < a.H_parts || grid > GMAX || grid % a.H_parts != 0 || grid / a.H_parts > a.X ||
+        a.n > INT32_MAX / 2)
+        return hipErrorInvalidValue;
+    switch (a.j) {
+#define VTK_BAND_J(J_)                                                                                           \
+    case J_:                                                                                                     \
+        hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        break;
+        VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
+        VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
+        VTK_BAND_J(14) VTK_BAND_J(15) VTK_BAND_J(16) VTK_BAND_J(17) VTK_BAND_J(18)
+#undef VTK_BAND_J
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Line-band DCGS2 step, wave-independent form (round 3, the default).  The same
+// sweep and the same arithmetic as k_band_step, cut differently:
+//  * a WAVEFRONT owns rows [v0, v0 + nrow) of the lines [xa, xb) of its line range (nrow <= 56:
+//    whole 8-row BJ blocks on lanes 0..nrow-1) and walks them with no workgroup barrier: lane
+//    nrow recomputes the v-halo row v0 + nrow and lane 63 the row v0 - 1 (p_j from the
+//    neighbour part's boundary copies, as before), so every SpMV gather of the part's rows
+//    comes from a per-wave LDS ring of 4 lines that the same wavefront writes (in-order LDS);
+//  * the dots are row-owned: a lane accumulates s = V^T p_{j+1} and |p|^2 for its row while it
+//    updates the line (V_k, v_j and p_{j+1} are in its registers then), keeps the line's V_k,
+//    v_j and p in registers across the next line's update and SpMV, and accumulates z = V^T w,
+//    p.w, |w|^2 once w of the line is known.  No dot operand goes through LDS, and the one
+//    workgroup barrier is the final reduction (per-wave DPP sums, then the waves in order);
+//  * a workgroup holds up to 8 parts of one line range (L = 800: 15 parts, two workgroups of 8
+//    and 7 waves), so most halo rows a wave recomputes were just read by its neighbour part on
+//    the same CU; the row-owned dots need 4 (j+1) doubles per lane (two waves per SIMD: <= 256
+//    VGPRs, one 8-wave workgroup per CU).
+// v_j, p_{j+1} and w are bit-identical to k_dc_update / k_sell (same operations, same order);
+// the dots are summed in another fixed order (deterministic).
+// ------------------------------------------------------------------------------------------
+constexpr int BW_MAXW = BAND_WAVE_MAXW;   // wavefronts per workgroup (2 per SIMD)
+
+template <int J>
+__global__ __launch_bounds__(BW_MAXW * 64) void k_band_wave(BandK a) {
+    constexpr int j = J;
+    constexpr int WU = 5;
+    __shared__ double ring_all[BW_MAXW * 4 * 64];
+    __shared__ double red[BW_MAXW * DC_NQ];
+    __shared__ double cs[BAND_JV], ce[BAND_JV];
+    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
+        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m);
+        return;
+    }
+    if (stopped(&a.st->stop_col, j)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, HW = (int)blockDim.x >> 6;
+    const int L = a.L, X = a.X, H = a.H_parts, GP = a.gp;
+    const int R = (int)gridDim.x / GP, rb = (int)blockIdx.x / GP;
+    const int h = ((int)blockIdx.x % GP) * HW + wv;   // the wave's part of the line
+    const bool wact = h < H;
+    const int NB = L >> 3;
+    const int blk0 = wact ? (int)((int64_t)h * NB / H) : 0, blk1 = wact ? (int)((int64_t)(h + 1) * NB / H) : 0;
+    const int v0 = 8 * blk0, nrow = 8 * (blk1 - blk0);
+    const bool own = wact && lane < nrow;
+    const bool rh = wact && lane == nrow && v0 + nrow < L;   // v-halo row after the part
+    const bool lh = wact && lane == 63 && v0 > 0;            // v-halo row before it
+    const bool upd = own || rh || lh;
+    const int v = own ? v0 + lane : (rh ? v0 + nrow : (lh ? v0 - 1 : v0));
+    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
+    const int nl = xb - xa;
+    const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
+    const int ii = lane & 7;
+    double *ring = ring_all + wv * 256;
+    for (int k = tid; k < j; k += (int)blockDim.x) {
+        cs[k] = a.cf->s[k];
+        ce[k] = a.cf->e[k];
+    }
+    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j];
+    __syncthreads();
+    // row-owned dot accumulators of step j+1: S[k] = V_k . p_{j+1}, Z[k] = V_k . w (k <= j, V_j = v_j)
+    double S[J + 1], Z[J + 1];
+    double aa = 0.0, ab = 0.0, ag = 0.0;
+#pragma unroll
+    for (int k = 0; k <= J; ++k) S[k] = Z[k] = 0.0;
+    double Vx[J + 1];   // V_k (k < j) and v_j of the previous line on the lane's row
+    double px = 0.0;    // p_{j+1} of the previous line on the lane's row
+#pragma unroll
+    for (int k = 0; k <= J; ++k) Vx[k] = 0.0;
+    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1)
+    auto line_of = [&](int it, int &kind) {
+        kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
+        return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
+    };
+    struct Ld {
+        double v[J > 0 ? J : 1];
+        double pj, wj;
+    };
+    // update operands of iteration it's line on the lane's row: V_k (k < j), p_j, w_j.  x-halo
+    // lines: p_j from the owner range's edge copy, or the ghost buffer across ranks; owned
+    // lines' v-halo rows: p_j from the neighbour part's boundary copy (the owners overwrite p_j
+    // in place with v_j)
+    auto load = [&](int it, Ld &o) {
+        int kind;
+        const int y = line_of(it, kind);
+        const int64_t row = (int64_t)y * L + v;
+        o.pj = 0.0;
+        o.wj = 0.0;
+        const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
+                               ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
+        if (upd) {
+            if (gh) {
+                o.pj = gh[(size_t)a.m * L + v];
+                o.wj = gh[(size_t)(a.m + 1) * L + v];
+            } else {
+                if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
+                else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
+                else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
+                else o.pj = a.vedge_in[((size_t)y * H + (lh ? h - 1 : h + 1)) * 2 + (lh ? 1 : 0)];
+                o.wj = __builtin_nontemporal_load(a.w_in + row);
+            }
+        }
+        if (gh) {
+#pragma unroll
+            for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < J; ++k) o.v[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
+        }
+    };
+    if (wact) {
+        for (int it = 0; it <= nl + 1; ++it) {
+            const int y = xa - 1 + it, x = y - 1;
+            const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
+            // the SpMV operands of line x (independent of the update): codes, dictionary, values, m
+            const int64_t lrow = (int64_t)(work ? x : xa) * L;
+            const int64_t row = lrow + v;
+            const int64_t q = row >> 6, q0 = (lrow + v0) >> 6;
+            const int l64 = (int)(row & 63);
+            uint32_t word = 0u;
+            int dv = 0;
+            double d[WU];
+            double mrow = 1.0;
+#pragma unroll
+            for (int k = 0; k < WU; ++k) d[k] = 0.0;
+            if (work) {
+                const int64_t qd = q0 + (lane >> 4);
+                dv = (lane < 32 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
+                if (own) {
+                    word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
+#pragma unroll
+                    for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
+                    mrow = __builtin_nontemporal_load(a.mtri + row);
+                }
+            }
+            // 1. update of line y (k_dc_update's operations); stores on owned lines
+            int kind;
+            const int yl = line_of(it, kind);
+            Ld cu;
+            load(it, cu);
+            const int64_t urow = (int64_t)yl * L + v;
+            double av = cu.pj, tv = cu.wj;
+#pragma unroll
+            for (int k = 0; k < J; ++k) {
+                const double sk = cs[k], ek = ce[k];
+                av = av - sk * cu.v[k];
+                tv = tv - ek * cu.v[k];
+            }
+            double vj = cu.pj;
+            if (j >= 1) vj = av * rinv;
+            tv = tv - ej * vj;
+            const double pn = tv * qc;
+            if (kind == 0 && own) {
+                if (j >= 1) __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + urow);
+                __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + urow);
+                if (yl == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
+                if (yl == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
+                if (H > 1 && lane == 0) a.vedge_out[((size_t)yl * H + h) * 2] = pn;
+                if (H > 1 && lane == nrow - 1) a.vedge_out[((size_t)yl * H + h) * 2 + 1] = pn;
+                // s = V_{j+1}^T p_{j+1} and |p|^2 on the lane's row of line y
+#pragma unroll
+                for (int k = 0; k < J; ++k) S[k] += cu.v[k] * pn;
+                S[J] += vj * pn;
+                aa += pn * pn;
+            }
+            if (upd) ring[(it & 3) * 64 + lane] = pn;
+            __builtin_amdgcn_wave_barrier();   // the wave's own LDS writes precede its reads (in-order LDS)
+            if (work) {
+                // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
+                double sacc = 0.0, sub = 0.0, sup = 0.0;
+                const int sel = (int)(q - q0) * 16;
+#pragma unroll
+                for (int k = 0; k < WU; ++k) {
+                    const int code = (int)((word >> (4 * k)) & 15u);
+                    const int off = __shfl(dv, (sel + code) & 63, 64);
+                    if (own && code != PK_CODES) {
+                        // the column's line relative to x and its position in that line, by range
+                        // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
+                        const int t = v + off;
+                        int rel, vc;
+                        const int c = x * L + t;
+                        if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
+                            const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
+                            rel = blk == a.left_blk ? -1 : 1;
+                            vc = kk - blk * L;
+                        } else if (t >= 0 && t < L) { rel = 0; vc = t; }
+                        else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
+                        else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
+                        else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
+                        else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
+                        const int sl = vc == v0 - 1 ? 63 : vc - v0;
+                        const double xv = ring[((x - xa + 1 + rel) & 3) * 64 + sl];
+                        sacc += d[k] * xv;
+                        if (off == -1 && ii > 0) sub = sub + d[k];
+                        if (off == 1 && ii < 7) sup = sup + d[k];
+                    }
+                }
+                const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
+                if (own) {
+                    __builtin_nontemporal_store(z, a.w_out + row);
+                    // 3. z = V_{j+1}^T w, p.w, |w|^2 on the lane's row of line x
+#pragma unroll
+                    for (int k = 0; k <= J; ++k) Z[k] += Vx[k] * z;
+                    ab += px * z;
+                    ag += z * z;
+                }
+            }
+            // line y's operands for its dots one line on
+#pragma unroll
+            for (int k = 0; k < J; ++k) Vx[k] = cu.v[k];
+            Vx[J] = vj;
+            px = pn;
+        }
+    }
+    // per-wave sums (fixed DPP tree), then the workgroup's waves in order: partials of step j+1
+    // in launch_dc_dots' layout
+    double *rw = red + wv * DC_NQ;
+#pragma unroll
+    for (int k = 0; k <= J; ++k) {
+        const double ts = wave_allsum(S[k]), tz = wave_allsum(Z[k]);
+        if (lane == 0) {
+            rw[k] = ts;
+            rw[DC_MAXJ + k] = tz;
+        }
+    }
+    {
+        const double t0 = wave_allsum(aa), t1 = wave_allsum(ab), t2 = wave_allsum(ag);
+        if (lane == 0) {
+            rw[2 * DC_MAXJ] = t0;
+            rw[2 * DC_MAXJ + 1] = t1;
+            rw[2 * DC_MAXJ + 2] = t2;
+        }
+    }
+    __syncthreads();
+    const int jn = j + 1;
+    for (int qq = tid; qq < DC_NQ; qq += (int)blockDim.x) {
+        const bool used = qq < jn || (qq >= DC_MAXJ && qq < DC_MAXJ + jn) || qq >= 2 * DC_MAXJ;
+        if (!used) continue;
+        double t = 0.0;
+        for (int w = 0; w < HW; ++w) t += red[w * DC_NQ + qq];
+        a.part[(size_t)qq * GMAX + blockIdx.x] = t;
+    }
+}
+
+hipError_t launch_band_wave(const BandK &a, int grid, int hw, int wu, hipStream_t s) {
+    if (wu != 5 || a.L % 8 != 0 || a.H_parts < 1 || a.gp < 1 || hw < 1 || hw > BW_MAXW || a.gp * hw < a.H_parts ||
+        a.j + 1 > BAND_JV || grid < a.gp || grid > GMAX || grid % a.gp != 0 || grid / a.gp > a.X / 2 ||
+        a.n > INT32_MAX / 2 || (int64_t)a.X * a.L != a.n)
+        return hipErrorInvalidValue;
+    switch (a.j) {
+#define VTK_BAND_J(J_)                                                                       \
+    case J_:                                                                                 \
+        hipLaunchKernelGGL((k_band_wave<J_>), dim3(grid), dim3(64 * hw), 0, s, a);           \
+        break;
+        VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
+        VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
+        VTK_BAND_J(14) VTK_BAND_J(15) VTK_BAND_J(16) VTK_BAND_J(17) VTK_BAND_J(18)
+#undef VTK_BAND_J
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ghost exchange of the distributed band step: pack the rank's first / last line
+// of v_{j-1} (V[j-1]; V[0] at j = 0), p_j (V[j]) and w_j into send pieces of 3 L, unpack the
+// received pieces into the ghost slots (v_{j-1} -> slot j-1 when j >= 1, p_j -> m, w_j -> m+1)
+__global__ __launch_bounds__(NT) void k_ghost_pack(const double *__restrict__ V, int64_t ld, int j,
+                                                   const double *__restrict__ w, int64_t n, int L,
+                                                   double *__restrict__ sbuf, int64_t off_first, int64_t off_last) {
+    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
+        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
+        const int64_t off = side == 0 ? off_first : off_last;
+        if (off < 0) continue;
+        const int64_t row = (side == 0 ? 0 : n - L) + t;
+        const double val = vec == 0 ? V[(size_t)(j >= 1 ? j - 1 : 0) * ld + row]
+                                    : (vec == 1 ? V[(size_t)j * ld + row] : w[row]);
+        sbuf[off + r] = val;
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_ghost_unpack(const double *__restrict__ rbuf, int64_t off_left, int64_t off_right,
+                                                     int j, int m, int L, double *__restrict__ ghost) {
+    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
+        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
+        const int64_t off = side == 0 ? off_left : off_right;
+        if (off < 0 || (vec == 0 && j == 0)) continue;
+        const int slot = vec == 0 ? j - 1 : m + vec - 1;
+        ghost[((size_t)side * (m + 2) + slot) * L + t] = rbuf[off + r];
+    }
+}
+
+hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,
+                             int64_t off_first, int64_t off_last, hipStream_t s) {
+    hipLaunchKernelGGL(k_ghost_pack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, V, ld, j, w, n, L, sbuf, off_first,
+                       off_last);
+    return hipGetLastError();
+}
+
+hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
+                               double *ghost, hipStream_t s) {
+    hipLaunchKernelGGL(k_ghost_unpack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, rbuf, off_left, off_right, j, m, L,
+                       ghost);
+    return hipGetLastError();
+}
+
+// distributed form of the check (local column numbering; the halo is exactly two neighbour lines,
+// halo block lblk the left one): an owned column within lines x-1..x+1 of the row's line without
+// wrap, a halo column only from the first (left block) or last (right block) local line
+__global__ __launch_bounds__(NT) void k_band_check_dist(const int32_t *__restrict__ indptr,
+                                                        const int32_t *__restrict__ indices, int64_t n, int L,
+                                                        int lblk, int *bad) {
+    const int64_t X = n / L;
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
+        const int64_t x = r / L, vr = r % L;
+        bool ok = true, vloc = true;
+        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
+            const int64_t c = indices[k];
+            int64_t vc;
+            if (c < 0 || c >= n + 2 * L) { ok = false; break; }
+            if (c < n) {
+                const int64_t rel = c / L - x;
+                if (rel < -1 || rel > 1) { ok = false; break; }
+                vc = c % L;
+            } else {
+                const int64_t kk = c - n, blk = kk / L;
+                if ((blk == lblk && x != 0) || (blk != lblk && x != X - 1)) { ok = false; break; }
+                vc = kk % L;
+            }
+            if (vc - vr < -1 || vc - vr > 1) vloc = false;
+        }
+        if (!ok) atomicOr(bad, 1);
+        if (!vloc) atomicOr(bad, 2);
+    }
+}
+
+hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
+                                  hipStream_t s) {
+    int64_t g = (n + NT - 1) / NT;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_band_check_dist, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, lblk, bad);
+    return hipGetLastError();
+}
+
+// *bad |= 1 when a column lies outside lines x-1..x+1 (mod X) of its row's line x; |= 2 when it
+// lies more than one row off the row's position v within its line
+__global__ __launch_bounds__(NT) void k_band_check(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
+                                                   int64_t n, int L, int X, int *bad) {
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
+        const int64_t x = r / L, vr = r % L;
+        bool ok = true, vloc = true;
+        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
+            const int64_t c = indices[k];
+            if (c < 0 || c >= n) { ok = false; break; }
+            int64_t rel = c / L - x;
+            if (rel > 1) rel -= X;
+            else if (rel < -1) rel += X;
+            if (rel < -1 || rel > 1) { ok = false; break; }
+            const int64_t dv = c % L - vr;
+            if (dv < -1 || dv > 1) vloc = false;
+        }
+        if (!ok) atomicOr(bad, 1);
+        if (!vloc) atomicOr(bad, 2);
+    }
+}
+
+hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
+                             hipStream_t s) {
+    int64_t g = (n + NT - 1) / NT;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(k_band_check, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, X, bad);
+    return hipGetLastError();
+}
+
+}  // namespace vtk

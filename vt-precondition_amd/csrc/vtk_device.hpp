@@ -1,0 +1,323 @@
+// vtk_device.hpp — device helpers shared by the gfx950 kernel translation units
+// (vtk_kernels.hip, vtk_band.hip): deterministic wave / workgroup reductions, DPP lane moves,
+// non-temporal load/store wrappers, the tridiagonal block-Jacobi group solves, the Hessenberg
+// back substitution and the DCGS2 x update.  Device code only; not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+
+#include "vtk_internal.hpp"
+
+namespace vtk {
+
+// ------------------------------------------------------------------------------------------
+// reductions
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_allsum(double v);
+__device__ __forceinline__ double wave_sum(double v) {
+    return wave_allsum(v);  // (every lane; callers read lane 0)
+}
+
+// every thread of the workgroup returns the same total (fixed order)
+__device__ __forceinline__ double block_sum(double v, double *red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+    return s;
+}
+
+// sum of p[i0], p[i0+STRIDE], ... (< cnt <= U*STRIDE) in that order, with every load issued
+// before the first add (a rolled loop paid one L2 round trip per element)
+template <int U, int STRIDE>
+__device__ __forceinline__ double strided_sum(const double *p, int cnt, int i0) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * STRIDE;
+        v[u] = i < cnt ? p[i] : 0.0;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+    return acc;
+}
+static_assert(GMAX <= 4 * NT && GMAX <= 16 * 64, "partial-sum unroll bounds");
+
+__device__ __forceinline__ double reduce_red(Red r, double *red) {
+    return block_sum(strided_sum<GMAX / NT, NT>(r.p, r.cnt, threadIdx.x), red);
+}
+
+__device__ __forceinline__ bool stopped(const int *stop_col, int col) {
+    // wave-uniform: one scalar load
+    return stop_col != nullptr && __builtin_nontemporal_load(stop_col) < col;
+}
+
+// The basis vector an MGS step subtracts (and the basis read by the x update) is loaded
+// non-temporal, 16 B per lane, so that w stays resident in the 256 MB Infinity Cache across
+// the chain of MGS kernels: on C3 (20M rows) an MGS step went from 122 us to 98 us
+// (tools/probe_mgs.hip).  Narrow (4/8 B) nt loads are slow on gfx950; the SpMV keeps plain loads.
+typedef double d2v __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T ldnt(const T *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ d2v ldnt2(const double *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+}
+// non-temporal vector stores (A/B: streamed-out results that are re-read only by a later
+// kernel gain; VTK_NT_MISC bits: 1 scale0 / x update (neutral, off), 2 SpMV epilogues (plain
+// SpMV 243 -> 223 us), 4 line apply (line solve +0.8 %))
+#ifndef VTK_NT_MISC
+#define VTK_NT_MISC 6
+#endif
+// non-temporal loads of operands read once per kernel (VTK_NT_LOADS bits: 1 fused BJ m,
+// 4 dots p/w, 8 line apply r/m; the update pass chooses per path, k_dc_update<NTPW>).
+// A/B: 1 = +2.5 % (C3 BJ path), 4|8 = +1 % (line path)
+#ifndef VTK_NT_LOADS
+#define VTK_NT_LOADS 13
+#endif
+template <int BIT>
+__device__ __forceinline__ double ld_nt(const double *p) {
+    if constexpr ((VTK_NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int BIT>
+__device__ __forceinline__ double2 ld_nt2(const double *p) {
+    if constexpr ((VTK_NT_LOADS & BIT) != 0) {
+        const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+        return make_double2(v.x, v.y);
+    } else {
+        return *reinterpret_cast<const double2 *>(p);
+    }
+}
+template <int BIT>
+__device__ __forceinline__ void st_nt(double *p, double v) {
+    if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <int BIT>
+__device__ __forceinline__ void st_nt2(double *p, double x, double y) {
+    if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(d2v{x, y}, reinterpret_cast<d2v *>(p));
+    else *reinterpret_cast<double2 *>(p) = make_double2(x, y);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// DPP lane moves (CDNA row-level data-parallel primitives: 16-lane rows, a VALU modifier
+// instead of an LDS-crossbar ds_bpermute).  Lanes whose source falls outside their row read 0.
+// Only the transport changes: a scan written with these moves does the same IEEE operations.
+// ------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+constexpr int DPP_ROW_SHL = 0x100;   // + n: lane i <- lane i + n of its row
+constexpr int DPP_ROW_SHR = 0x110;   // + n: lane i <- lane i - n of its row
+// __shfl_up / __shfl_down within groups of W <= 16 lanes (W divides 16): the lanes a group
+// would take from outside itself are exactly those the callers mask off
+template <int W>
+__device__ __forceinline__ double grp_up(double v, int off) {
+    if constexpr (W <= 16) {
+        switch (off) {
+            case 1: return dpp_mov<DPP_ROW_SHR + 1>(v);
+            case 2: return dpp_mov<DPP_ROW_SHR + 2>(v);
+            case 4: return dpp_mov<DPP_ROW_SHR + 4>(v);
+            default: return dpp_mov<DPP_ROW_SHR + 8>(v);
+        }
+    } else {
+        return __shfl_up(v, off, W);
+    }
+}
+template <int W>
+__device__ __forceinline__ double grp_down(double v, int off) {
+    if constexpr (W <= 16) {
+        switch (off) {
+            case 1: return dpp_mov<DPP_ROW_SHL + 1>(v);
+            case 2: return dpp_mov<DPP_ROW_SHL + 2>(v);
+            case 4: return dpp_mov<DPP_ROW_SHL + 4>(v);
+            default: return dpp_mov<DPP_ROW_SHL + 8>(v);
+        }
+    } else {
+        return __shfl_down(v, off, W);
+    }
+}
+
+// Block-Jacobi apply with tridiagonal blocks, BS lanes per block (one row each): the LU solve
+// L d = y, U z = d as two affine scans over the group (log2 BS shuffle steps each):
+//   d_i = y_i - l_i d_{i-1},   z_i = m_i d_i - g_i z_{i+1}   (m_i = 1/u_i, g_i = sup_i / u_i)
+// Same M^-1 as the inverse rows to rounding; 24 B per row instead of 8 BS.
+template <int BS>
+__device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, int lane, const double *tri,
+                                               int64_t ld) {
+    const int ii = lane & (BS - 1);
+    double l = 0.0, m = 1.0, g = 0.0;
+    if (act) {
+        l = tri[row];
+        m = tri[ld + row];
+        g = tri[2 * ld + row];
+    }
+    double A = y, B = -l;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double Ap = grp_up<BS>(A, off), Bp = grp_up<BS>(B, off);
+        if (ii >= off) {
+            A = A + B * Ap;
+            B = B * Bp;
+        }
+    }
+    A = m * A;
+    B = -g;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double An = grp_down<BS>(A, off), Bn = grp_down<BS>(B, off);
+        if (ii + off < BS) {
+            A = A + B * An;
+            B = B * Bn;
+        }
+    }
+    return A;
+}
+
+// The same solve from m alone (SELL kernels): the lane has its row's block sub/super-diagonal
+// entries from the SpMV loop (duplicates summed in stored order, as in the setup), so
+// l_i = sub_i m_{i-1} (m_{i-1} from the neighbour lane) and g_i = sup_i m_i: 8 B per row.
+template <int BS>
+__device__ __forceinline__ double bj_trim_group(double y, int lane, double sub, double sup, double m) {
+    const int ii = lane & (BS - 1);
+    const double mprev = grp_up<BS>(m, 1);
+    const double l = ii > 0 ? sub * mprev : 0.0;
+    const double g = sup * m;
+    double A = y, B = -l;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double Ap = grp_up<BS>(A, off), Bp = grp_up<BS>(B, off);
+        if (ii >= off) {
+            A = A + B * Ap;
+            B = B * Bp;
+        }
+    }
+    A = m * A;
+    B = -g;
+#pragma unroll
+    for (int off = 1; off < BS; off <<= 1) {
+        const double An = grp_down<BS>(A, off), Bn = grp_down<BS>(B, off);
+        if (ii + off < BS) {
+            A = A + B * An;
+            B = B * Bn;
+        }
+    }
+    return A;
+}
+
+// ------------------------------------------------------------------------------------------
+// wave reductions by DPP moves and readlanes
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+// sum over the wavefront, the same bits in every lane: xor-1/xor-2 quad permutes, half-row and
+// row mirrors (each step adds a lane pair that both end up equal, a + b = b + a), then the four
+// row sums in a fixed order.  DPP moves and readlanes: no LDS traffic.
+__device__ __forceinline__ double wave_allsum(double v) {
+    v = v + dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = v + dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = v + dpp_mov<0x141>(v);   // row_half_mirror
+    v = v + dpp_mov<0x140>(v);   // row_mirror
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+// ------------------------------------------------------------------------------------------
+// x += y @ V[0..col] with y from the (m+1) x m Hessenberg least squares
+// (iterative.py:799-814).  Workgroup-redundant triangular solve on lane 0, into LDS.
+// ------------------------------------------------------------------------------------------
+// y = H^-1 S over columns 0..col (lane 0 of a workgroup, into LDS ys; iterative.py:799-812)
+__device__ inline void hess_solve(const double *__restrict__ H, const double *__restrict__ S, int m, int col,
+                                  double *ys) {
+    const int M1 = m + 1;
+    for (int k = 0; k <= col; ++k) ys[k] = S[k];
+    if (H[(size_t)col * M1 + col] == 0.0) ys[col] = 0.0;
+    for (int k = col; k > 0; --k) {
+        if (ys[k] != 0.0) {
+            ys[k] = ys[k] / H[(size_t)k * M1 + k];
+            const double t = ys[k];
+            for (int i = 0; i < k; ++i) ys[i] = ys[i] - t * H[(size_t)k * M1 + i];
+        }
+    }
+    if (ys[0] != 0.0) ys[0] = ys[0] / H[0];
+}
+
+// v_j = (p_j - sum_k s_k v_k) / r  (in place, j >= 1);  p_{j+1} = (w - sum_k e_k v_k - e_j v_j) * q
+#ifndef VTK_UPD_NT
+#define VTK_UPD_NT 2   // non-temporal stores in the update pass: 1 v_j, 2 v_j and p_{j+1} (A/B: 2 = +2.6 % it/s)
+#endif
+#ifndef VTK_XUP_FUSED
+#define VTK_XUP_FUSED 1   // the cycle's x update inside the stopping step's update pass (one basis read less per cycle)
+#endif
+// The cycle's x update in the update pass of the step whose scalar kernel stopped it (xup_tag):
+// c = stop_col is j-1 (column j-1 finalised in step j: V[0..j-1] all stored) or j (column j
+// committed early: v_j = (p_j - V_j s) / r formed here exactly as the normal pass would store
+// it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
+static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
+                                        const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
+                                        const double *__restrict__ S, int m) {
+    __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ];
+    __shared__ double rinv_s;
+    if (threadIdx.x == 0) {
+        hess_solve(H, S, m, c, ys);
+        rinv_s = cf->rinv;
+    }
+    if (c == j)
+        for (int k = threadIdx.x; k < j; k += blockDim.x) cs[k] = cf->s[k];
+    __syncthreads();
+    const double rinv = rinv_s;
+    const double *pj = V + (size_t)j * ld;
+    const int kv = c == j ? j : c + 1;   // stored basis vectors in the sum
+    const int64_t stride = 2 * (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += stride) {
+        if (i + 1 < n) {
+            double ax = 0.0, ay = 0.0;
+            double2 a = make_double2(0.0, 0.0);
+            if (c == j) {
+                const d2v pp = ldnt2(pj + i);
+                a = make_double2(pp.x, pp.y);
+            }
+            for (int k = 0; k < kv; ++k) {
+                const d2v v = ldnt2(V + (size_t)k * ld + i);
+                ax += ys[k] * v.x;
+                ay += ys[k] * v.y;
+                if (c == j) {
+                    const double sk = cs[k];
+                    a.x = a.x - sk * v.x;
+                    a.y = a.y - sk * v.y;
+                }
+            }
+            if (c == j) {
+                const double vx = j >= 1 ? a.x * rinv : a.x, vy = j >= 1 ? a.y * rinv : a.y;
+                ax += ys[j] * vx;
+                ay += ys[j] * vy;
+            }
+            double2 xv = *reinterpret_cast<const double2 *>(x + i);
+            xv.x = xv.x + ax;
+            xv.y = xv.y + ay;
+            st_nt2<1>(x + i, xv.x, xv.y);
+        } else {
+            double ax = 0.0, a = c == j ? pj[i] : 0.0;
+            for (int k = 0; k < kv; ++k) {
+                const double v = V[(size_t)k * ld + i];
+                ax += ys[k] * v;
+                if (c == j) a = a - cs[k] * v;
+            }
+            if (c == j) ax += ys[j] * (j >= 1 ? a * rinv : a);
+            x[i] = x[i] + ax;
+        }
+    }
+}
+
+}  // namespace vtk

@@ -344,9 +344,9 @@ hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64
                             const DcCoef *cf, int grid, const GmresState *st, double *x,
                             const double *H, const double *S, int m, int nt_pw, hipStream_t s);
 
-// Line-band DCGS2 step (k_band_step): update pass of step j + SpMV, tridiagonal BJ(8) and
-// dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded columns,
-// fp64 values; single rank).  grid workgroups (<= X lines, <= GMAX), partials of step j+1 in
+// Line-band DCGS2 step (k_band_wave / k_band_step): update pass of step j + SpMV, tridiagonal
+// BJ(8) and dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded
+// columns, fp64 values; across ranks through the ghost lines).  grid workgroups (<= X lines, <= GMAX), partials of step j+1 in
 // the launch_dc_dots layout; edge_in / edge_out: [grid][2][L] first/last-line copies of p.
 struct BandK {
     const uint32_t *pk;
@@ -372,9 +372,15 @@ struct BandK {
     const double *ghost;         // distributed: [2][m+2][L] the left / right neighbour lines'
                                  // v_k (k < j), p_j, w_j (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
-    uint64_t lmagic;   // floor(c / L) = (c * lmagic) >> 40 for c < 2^40 / L
+    int gp = 1;                  // k_band_wave: workgroups per line range (grid = ranges x gp)
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
+// wave-independent form (k_band_wave, the default): parts of <= 56 rows per wavefront, hw
+// wavefronts per workgroup, a.gp workgroups per line range (band_wave_plan)
+constexpr int BAND_WAVE_ROWS = 56;   // rows a wavefront owns (7 BJ blocks; lanes 56 / 63: v-halo rows)
+constexpr int BAND_WAVE_MAXW = 8;    // wavefronts per workgroup (two per SIMD: <= 256 VGPRs)
+bool band_wave_plan(int64_t L, int *H, int *gp, int *hw);   // vtk_host.cpp
+hipError_t launch_band_wave(const BandK &a, int grid, int hw, int wu, hipStream_t s);
 hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
                                   hipStream_t s);
 hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,

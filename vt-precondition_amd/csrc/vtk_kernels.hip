@@ -19,102 +19,9 @@
 
 #include "vtk_internal.hpp"
 #include "vtk_vlasov.hpp"
+#include "vtk_device.hpp"
 
 namespace vtk {
-
-// ------------------------------------------------------------------------------------------
-// reductions
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_allsum(double v);
-__device__ __forceinline__ double wave_sum(double v) {
-    return wave_allsum(v);  // (every lane; callers read lane 0)
-}
-
-// every thread of the workgroup returns the same total (fixed order)
-__device__ __forceinline__ double block_sum(double v, double *red) {
-    v = wave_sum(v);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __syncthreads();
-    if (lane == 0) red[wid] = v;
-    __syncthreads();
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < NT / 64; ++i) s += red[i];
-    return s;
-}
-
-// sum of p[i0], p[i0+STRIDE], ... (< cnt <= U*STRIDE) in that order, with every load issued
-// before the first add (a rolled loop paid one L2 round trip per element)
-template <int U, int STRIDE>
-__device__ __forceinline__ double strided_sum(const double *p, int cnt, int i0) {
-    double v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * STRIDE;
-        v[u] = i < cnt ? p[i] : 0.0;
-    }
-    double acc = 0.0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc += v[u];
-    return acc;
-}
-static_assert(GMAX <= 4 * NT && GMAX <= 16 * 64, "partial-sum unroll bounds");
-
-__device__ __forceinline__ double reduce_red(Red r, double *red) {
-    return block_sum(strided_sum<GMAX / NT, NT>(r.p, r.cnt, threadIdx.x), red);
-}
-
-__device__ __forceinline__ bool stopped(const int *stop_col, int col) {
-    // wave-uniform: one scalar load
-    return stop_col != nullptr && __builtin_nontemporal_load(stop_col) < col;
-}
-
-// The basis vector an MGS step subtracts (and the basis read by the x update) is loaded
-// non-temporal, 16 B per lane, so that w stays resident in the 256 MB Infinity Cache across
-// the chain of MGS kernels: on C3 (20M rows) an MGS step went from 122 us to 98 us
-// (tools/probe_mgs.hip).  Narrow (4/8 B) nt loads are slow on gfx950; the SpMV keeps plain loads.
-typedef double d2v __attribute__((ext_vector_type(2)));
-template <typename T>
-__device__ __forceinline__ T ldnt(const T *p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ d2v ldnt2(const double *p) {
-    return __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
-}
-// non-temporal vector stores (A/B: streamed-out results that are re-read only by a later
-// kernel gain; VTK_NT_MISC bits: 1 scale0 / x update (neutral, off), 2 SpMV epilogues (plain
-// SpMV 243 -> 223 us), 4 line apply (line solve +0.8 %))
-#ifndef VTK_NT_MISC
-#define VTK_NT_MISC 6
-#endif
-// non-temporal loads of operands read once per kernel (VTK_NT_LOADS bits: 1 fused BJ m,
-// 4 dots p/w, 8 line apply r/m; the update pass chooses per path, k_dc_update<NTPW>).
-// A/B: 1 = +2.5 % (C3 BJ path), 4|8 = +1 % (line path)
-#ifndef VTK_NT_LOADS
-#define VTK_NT_LOADS 13
-#endif
-template <int BIT>
-__device__ __forceinline__ double ld_nt(const double *p) {
-    if constexpr ((VTK_NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <int BIT>
-__device__ __forceinline__ double2 ld_nt2(const double *p) {
-    if constexpr ((VTK_NT_LOADS & BIT) != 0) {
-        const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
-        return make_double2(v.x, v.y);
-    } else {
-        return *reinterpret_cast<const double2 *>(p);
-    }
-}
-template <int BIT>
-__device__ __forceinline__ void st_nt(double *p, double v) {
-    if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-template <int BIT>
-__device__ __forceinline__ void st_nt2(double *p, double x, double y) {
-    if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(d2v{x, y}, reinterpret_cast<d2v *>(p));
-    else *reinterpret_cast<double2 *>(p) = make_double2(x, y);
-}
 
 // ------------------------------------------------------------------------------------------
 // CSR SpMV, CSR-stream tiles: a workgroup stages one tile's products val*x[col] in LDS with
@@ -159,47 +66,6 @@ __device__ __forceinline__ double xload(const SpmvK<VT, HALO> &a, int c) {
     return a.x[c];
 }
 
-// ------------------------------------------------------------------------------------------
-// DPP lane moves (CDNA row-level data-parallel primitives: 16-lane rows, a VALU modifier
-// instead of an LDS-crossbar ds_bpermute).  Lanes whose source falls outside their row read 0.
-// Only the transport changes: a scan written with these moves does the same IEEE operations.
-// ------------------------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
-    return __hiloint2double(hi, lo);
-}
-constexpr int DPP_ROW_SHL = 0x100;   // + n: lane i <- lane i + n of its row
-constexpr int DPP_ROW_SHR = 0x110;   // + n: lane i <- lane i - n of its row
-// __shfl_up / __shfl_down within groups of W <= 16 lanes (W divides 16): the lanes a group
-// would take from outside itself are exactly those the callers mask off
-template <int W>
-__device__ __forceinline__ double grp_up(double v, int off) {
-    if constexpr (W <= 16) {
-        switch (off) {
-            case 1: return dpp_mov<DPP_ROW_SHR + 1>(v);
-            case 2: return dpp_mov<DPP_ROW_SHR + 2>(v);
-            case 4: return dpp_mov<DPP_ROW_SHR + 4>(v);
-            default: return dpp_mov<DPP_ROW_SHR + 8>(v);
-        }
-    } else {
-        return __shfl_up(v, off, W);
-    }
-}
-template <int W>
-__device__ __forceinline__ double grp_down(double v, int off) {
-    if constexpr (W <= 16) {
-        switch (off) {
-            case 1: return dpp_mov<DPP_ROW_SHL + 1>(v);
-            case 2: return dpp_mov<DPP_ROW_SHL + 2>(v);
-            case 4: return dpp_mov<DPP_ROW_SHL + 4>(v);
-            default: return dpp_mov<DPP_ROW_SHL + 8>(v);
-        }
-    } else {
-        return __shfl_down(v, off, W);
-    }
-}
 
 template <int BS>
 __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]) {
@@ -216,72 +82,6 @@ __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]
     }
 }
 
-// Block-Jacobi apply with tridiagonal blocks, BS lanes per block (one row each): the LU solve
-// L d = y, U z = d as two affine scans over the group (log2 BS shuffle steps each):
-//   d_i = y_i - l_i d_{i-1},   z_i = m_i d_i - g_i z_{i+1}   (m_i = 1/u_i, g_i = sup_i / u_i)
-// Same M^-1 as the inverse rows to rounding; 24 B per row instead of 8 BS.
-template <int BS>
-__device__ __forceinline__ double bj_tri_group(double y, bool act, int64_t row, int lane, const double *tri,
-                                               int64_t ld) {
-    const int ii = lane & (BS - 1);
-    double l = 0.0, m = 1.0, g = 0.0;
-    if (act) {
-        l = tri[row];
-        m = tri[ld + row];
-        g = tri[2 * ld + row];
-    }
-    double A = y, B = -l;
-#pragma unroll
-    for (int off = 1; off < BS; off <<= 1) {
-        const double Ap = grp_up<BS>(A, off), Bp = grp_up<BS>(B, off);
-        if (ii >= off) {
-            A = A + B * Ap;
-            B = B * Bp;
-        }
-    }
-    A = m * A;
-    B = -g;
-#pragma unroll
-    for (int off = 1; off < BS; off <<= 1) {
-        const double An = grp_down<BS>(A, off), Bn = grp_down<BS>(B, off);
-        if (ii + off < BS) {
-            A = A + B * An;
-            B = B * Bn;
-        }
-    }
-    return A;
-}
-
-// The same solve from m alone (SELL kernels): the lane has its row's block sub/super-diagonal
-// entries from the SpMV loop (duplicates summed in stored order, as in the setup), so
-// l_i = sub_i m_{i-1} (m_{i-1} from the neighbour lane) and g_i = sup_i m_i: 8 B per row.
-template <int BS>
-__device__ __forceinline__ double bj_trim_group(double y, int lane, double sub, double sup, double m) {
-    const int ii = lane & (BS - 1);
-    const double mprev = grp_up<BS>(m, 1);
-    const double l = ii > 0 ? sub * mprev : 0.0;
-    const double g = sup * m;
-    double A = y, B = -l;
-#pragma unroll
-    for (int off = 1; off < BS; off <<= 1) {
-        const double Ap = grp_up<BS>(A, off), Bp = grp_up<BS>(B, off);
-        if (ii >= off) {
-            A = A + B * Ap;
-            B = B * Bp;
-        }
-    }
-    A = m * A;
-    B = -g;
-#pragma unroll
-    for (int off = 1; off < BS; off <<= 1) {
-        const double An = grp_down<BS>(A, off), Bn = grp_down<BS>(B, off);
-        if (ii + off < BS) {
-            A = A + B * An;
-            B = B * Bn;
-        }
-    }
-    return A;
-}
 
 // Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
 // 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
@@ -558,21 +358,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // ~360 us + 29 us per register vector.  Tried and measured slower on one box (A/B): 20
 // register vectors at 3 waves/SIMD (-2 %), k >= 10 handed to k_dc_dots (-3 %).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-// sum over the wavefront, the same bits in every lane: xor-1/xor-2 quad permutes, half-row and
-// row mirrors (each step adds a lane pair that both end up equal, a + b = b + a), then the four
-// row sums in a fixed order.  DPP moves and readlanes: no LDS traffic.
-__device__ __forceinline__ double wave_allsum(double v) {
-    v = v + dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
-    v = v + dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
-    v = v + dpp_mov<0x141>(v);   // row_half_mirror
-    v = v + dpp_mov<0x140>(v);   // row_mirror
-    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
-}
 
 #ifndef VTK_DC_KB
 #define VTK_DC_KB 4
@@ -2319,21 +2104,6 @@ hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresSt
 // x += y @ V[0..col] with y from the (m+1) x m Hessenberg least squares
 // (iterative.py:799-814).  Workgroup-redundant triangular solve on lane 0, into LDS.
 // ------------------------------------------------------------------------------------------
-// y = H^-1 S over columns 0..col (lane 0 of a workgroup, into LDS ys; iterative.py:799-812)
-__device__ inline void hess_solve(const double *__restrict__ H, const double *__restrict__ S, int m, int col,
-                                  double *ys) {
-    const int M1 = m + 1;
-    for (int k = 0; k <= col; ++k) ys[k] = S[k];
-    if (H[(size_t)col * M1 + col] == 0.0) ys[col] = 0.0;
-    for (int k = col; k > 0; --k) {
-        if (ys[k] != 0.0) {
-            ys[k] = ys[k] / H[(size_t)k * M1 + k];
-            const double t = ys[k];
-            for (int i = 0; i < k; ++i) ys[i] = ys[i] - t * H[(size_t)k * M1 + i];
-        }
-    }
-    if (ys[0] != 0.0) ys[0] = ys[0] / H[0];
-}
 
 __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, const double *__restrict__ S,
                                                 const double *__restrict__ V, int64_t ld,
@@ -2923,72 +2693,6 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
     return hipGetLastError();
 }
 
-// v_j = (p_j - sum_k s_k v_k) / r  (in place, j >= 1);  p_{j+1} = (w - sum_k e_k v_k - e_j v_j) * q
-#ifndef VTK_UPD_NT
-#define VTK_UPD_NT 2   // non-temporal stores in the update pass: 1 v_j, 2 v_j and p_{j+1} (A/B: 2 = +2.6 % it/s)
-#endif
-#ifndef VTK_XUP_FUSED
-#define VTK_XUP_FUSED 1   // the cycle's x update inside the stopping step's update pass (one basis read less per cycle)
-#endif
-// The cycle's x update in the update pass of the step whose scalar kernel stopped it (xup_tag):
-// c = stop_col is j-1 (column j-1 finalised in step j: V[0..j-1] all stored) or j (column j
-// committed early: v_j = (p_j - V_j s) / r formed here exactly as the normal pass would store
-// it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
-__device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
-                                        const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
-                                        const double *__restrict__ S, int m) {
-    __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ];
-    __shared__ double rinv_s;
-    if (threadIdx.x == 0) {
-        hess_solve(H, S, m, c, ys);
-        rinv_s = cf->rinv;
-    }
-    if (c == j)
-        for (int k = threadIdx.x; k < j; k += blockDim.x) cs[k] = cf->s[k];
-    __syncthreads();
-    const double rinv = rinv_s;
-    const double *pj = V + (size_t)j * ld;
-    const int kv = c == j ? j : c + 1;   // stored basis vectors in the sum
-    const int64_t stride = 2 * (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += stride) {
-        if (i + 1 < n) {
-            double ax = 0.0, ay = 0.0;
-            double2 a = make_double2(0.0, 0.0);
-            if (c == j) {
-                const d2v pp = ldnt2(pj + i);
-                a = make_double2(pp.x, pp.y);
-            }
-            for (int k = 0; k < kv; ++k) {
-                const d2v v = ldnt2(V + (size_t)k * ld + i);
-                ax += ys[k] * v.x;
-                ay += ys[k] * v.y;
-                if (c == j) {
-                    const double sk = cs[k];
-                    a.x = a.x - sk * v.x;
-                    a.y = a.y - sk * v.y;
-                }
-            }
-            if (c == j) {
-                const double vx = j >= 1 ? a.x * rinv : a.x, vy = j >= 1 ? a.y * rinv : a.y;
-                ax += ys[j] * vx;
-                ay += ys[j] * vy;
-            }
-            double2 xv = *reinterpret_cast<const double2 *>(x + i);
-            xv.x = xv.x + ax;
-            xv.y = xv.y + ay;
-            st_nt2<1>(x + i, xv.x, xv.y);
-        } else {
-            double ax = 0.0, a = c == j ? pj[i] : 0.0;
-            for (int k = 0; k < kv; ++k) {
-                const double v = V[(size_t)k * ld + i];
-                ax += ys[k] * v;
-                if (c == j) a = a - cs[k] * v;
-            }
-            if (c == j) ax += ys[j] * (j >= 1 ? a * rinv : a);
-            x[i] = x[i] + ax;
-        }
-    }
-}
 
 // NTPW: p_j and w loaded non-temporal (A/B: +2 % on the unfused (line) path, -1 % after the
 // fused BJ step, whose w the update re-reads warm)
@@ -3082,444 +2786,5 @@ int vector_grid(int64_t n) {
 }
 
 
-// ------------------------------------------------------------------------------------------
-// Line-band DCGS2 step.  For an operator whose rows form x-lines of L rows
-// (row = x L + v) with every column in lines x-1, x, x+1 (periodic in x) at v-1..v+1 -- the 2D
-// Vlasov operators, L = Nv -- the update pass of step j and the fused SpMV + BJ + dots of step
-// j+1 run as ONE sweep.  Workgroup (range r, part h) owns rows v0 <= v < v0 + LP (LP = L / H)
-// of the lines [xa, xb) of range r and walks them in order; at line x it
-//   1. updates line x+1 (v_j, p_{j+1} exactly as k_dc_update) on its rows plus one v-halo row
-//      on each side, and puts p_{j+1}(x+1) into an LDS ring of 4 lines,
-//   2. computes w(x) = M^-1 A p_{j+1} on its rows of line x from the ring (the SELL entries in
-//      stored order and the tridiagonal BJ solve exactly as k_sell: w is bit-identical),
-//   3. accumulates step j+1's dots s = V_{j+1}^T p_{j+1}, z = V_{j+1}^T w, |p|^2, p.w, |w|^2
-//      from LDS: the line's basis rows were staged there by step 1 one line earlier.
-// The basis is read from HBM once per step instead of twice (update pass + dots), p_{j+1} is
-// never re-read for the SpMV gathers, and one launch replaces two.  Rows another workgroup owns
-// are recomputed: the x-halo lines xa-1 and xb (their p_j from the owner's copy of its first /
-// last line from the previous step -- the owner overwrites p_j in place with v_j) and the
-// v-halo rows v0-1, v0+LP (p_j from the owner's per-line boundary copies).  7 waves; lane
-// tid <-> row v = v0 - 8 + tid (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two
-// workgroups per CU, whose update / SpMV / dots phases overlap.
-// ------------------------------------------------------------------------------------------
-constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
-// geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
-// 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU)
-template <int GEO> struct BandGeo;
-template <> struct BandGeo<2> { static constexpr int LP = 400, T = 448, WPC = 2; };
-template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4; };
-#ifndef VTK_BAND_GEO
-#define VTK_BAND_GEO 2
-#endif
-#ifndef VTK_BAND_DOTS_UNROLL
-#define VTK_BAND_DOTS_UNROLL 2   // the dots' 64-row passes issued together (LDS latency once per group)
-#endif
-#ifndef VTK_BAND_REREAD
-#define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
-#endif
-#ifndef VTK_BAND_PF
-#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 8)   // j <= this: next line's update operands prefetched across SpMV + dots
-#endif
-#ifndef VTK_BAND_VBUF_FIXED
-#define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
-#endif
-
-template <int WU, int J, int GEO>
-__global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
-    constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
-    constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
-    __shared__ double vbuf[VTK_BAND_REREAD ? 1 : (VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
-    __shared__ double ring[4 * BAND_RS];
-    __shared__ double wbuf[BAND_LP];
-    __shared__ double red[DC_NQ];
-    __shared__ double cs[BAND_JV], ce[BAND_JV];
-    constexpr int j = J;
-    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
-        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m);
-        return;
-    }
-    if (stopped(&a.st->stop_col, j)) return;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int L = a.L, X = a.X, H = a.H_parts, LP = L / H;
-    const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
-    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
-    const int v = v0 - 8 + tid;
-    const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
-    const bool own = tid >= 8 && tid < 8 + LP;
-    const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
-    const int ii = lane & 7;
-    for (int k = tid; k < j; k += BAND_T) {
-        cs[k] = a.cf->s[k];
-        ce[k] = a.cf->e[k];
-    }
-    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j];
-    __syncthreads();
-    double vreg[J + 1];
-    double acc[BAND_IT][3];
-#pragma unroll
-    for (int u = 0; u < BAND_IT; ++u) acc[u][0] = acc[u][1] = acc[u][2] = 0.0;
-    // update of line y on the lane's row: kind 0 an owned line, 1 / 2 the x-halo line before xa /
-    // after xb-1 (p_j from the owner's edge copy; nothing stored); owned lines' v-halo rows take
-    // p_j from the neighbour part's boundary copy.  vreg = V_k(y) k < j, then v_j.
-    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1)
-    const int nl = xb - xa;
-    auto line_of = [&](int it, int &kind) {
-        kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
-        return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
-    };
-    // update operands of iteration it's line on the lane's row: V_k (k < j), p_j, w_j.  kind 1 / 2
-    // (x-halo lines): p_j from the owner's edge copy; owned lines' v-halo rows: p_j from the
-    // neighbour part's boundary copy (the owners overwrite p_j in place with v_j)
-    struct Ld {
-        double v[J > 0 ? J : 1];
-        double pj, wj;
-    };
-    auto load = [&](int it, Ld &o) {
-        int kind;
-        const int y = line_of(it, kind);
-        const int64_t row = (int64_t)y * L + (upd ? v : 0);
-        o.pj = 0.0;
-        o.wj = 0.0;
-        // a rank's first / last line range: the x-halo line is a neighbour rank's line, whose
-        // V_k, p_j, w_j arrived in the ghost buffer (slots k, m, m + 1)
-        const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
-                               ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
-        if (upd) {
-            if (gh) {
-                o.pj = gh[(size_t)a.m * L + v];
-                o.wj = gh[(size_t)(a.m + 1) * L + v];
-            } else {
-                if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
-                else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
-                else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
-                else o.pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
-                o.wj = __builtin_nontemporal_load(a.w_in + row);
-            }
-        }
-        if (gh) {
-#pragma unroll
-            for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
-        } else {
-#pragma unroll
-            for (int k = 0; k < J; ++k)
-                o.v[k] = upd ? (VTK_BAND_REREAD ? a.V[(size_t)k * a.ld + row]
-                                                : __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row)) : 0.0;
-        }
-    };
-    // the update itself (k_dc_update's operations); stores on owned lines; vreg = V_k, v_j
-    auto update = [&](int it, const Ld &o) -> double {
-        int kind;
-        const int y = line_of(it, kind);
-        const int64_t row = (int64_t)y * L + (upd ? v : 0);
-#pragma unroll
-        for (int k = 0; k < J; ++k) vreg[k] = o.v[k];
-        double av = o.pj, tv = o.wj;
-#pragma unroll
-        for (int k = 0; k < J; ++k) {
-            const double sk = cs[k], ek = ce[k];
-            av = av - sk * vreg[k];
-            tv = tv - ek * vreg[k];
-        }
-        double vj = o.pj;
-        if (j >= 1) vj = av * rinv;
-        tv = tv - ej * vj;
-        const double pn = tv * qc;
-        vreg[J] = vj;
-        if (kind == 0 && own) {
-            if (j >= 1) {
-                if constexpr (VTK_BAND_REREAD) a.V[(size_t)j * a.ld + row] = vj;
-                else __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
-            }
-            __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
-            if (y == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
-            if (y == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
-            if (H > 1 && tid == 8) a.vedge_out[((size_t)y * H + h) * 2] = pn;
-            if (H > 1 && tid == 7 + LP) a.vedge_out[((size_t)y * H + h) * 2 + 1] = pn;
-        }
-        return pn;
-    };
-    auto stage = [&]() {
-        if (!VTK_BAND_REREAD && own) {
-#pragma unroll
-            for (int k = 0; k <= J; ++k) vbuf[k * BAND_LP + tid - 8] = vreg[k];
-        }
-    };
-    auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
-    // iteration it updates line y = xa - 1 + it and, from it = 2 on, runs the SpMV and dots of
-    // line y - 1.  PF (small j, registers allow): the next line's update operands are loaded
-    // during this line's SpMV and dots (software pipeline)
-    constexpr bool PF = J <= VTK_BAND_PF;
-    Ld nx;
-    if constexpr (PF) load(0, nx);
-    for (int it = 0; it <= nl + 1; ++it) {
-        const int y = xa - 1 + it, x = y - 1;
-        const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
-        const int64_t lrow = (int64_t)(work ? x : xa) * L;
-        const int64_t row = lrow + (own ? v : v0);
-        // the SpMV operands of line x (independent of the update): codes, dictionary, values, m
-        const int64_t q = row >> 6, q0 = (lrow + v0 - 8 + 64 * wv) >> 6;
-        const int l64 = (int)(row & 63);
-        uint32_t word = 0u;
-        int dv = 0;
-        double d[WU];
-        double mrow = 1.0;
-        if (work) {
-            word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
-            const int64_t qd = q0 + (lane >> 4);
-            dv = (lane < 32 && qd >= 0 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
-#pragma unroll
-            for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
-            if (own) mrow = __builtin_nontemporal_load(a.mtri + row);
-        }
-        // 1. update of line y
-        {
-            Ld cu;
-            if constexpr (PF) cu = nx;
-            else load(it, cu);
-            const double pn = update(it, cu);
-            if (upd) ring[slot(y) + tid] = pn;
-            if constexpr (PF) {
-                if (it <= nl) load(it + 1, nx);
-            }
-        }
-        __syncthreads();
-        if (work) {
-            // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
-            double sacc = 0.0, sub = 0.0, sup = 0.0;
-            const int sel = (int)(q - q0) * 16;
-#pragma unroll
-            for (int k = 0; k < WU; ++k) {
-                const int code = (int)((word >> (4 * k)) & 15u);
-                const int off = __shfl(dv, (sel + code) & 63, 64);
-                if (own && code != PK_CODES) {
-                    // the column's line relative to x and its position in that line, by range
-                    // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
-                    const int t = v + off;
-                    int rel, vc;
-                    const int c = x * L + t;
-                    if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
-                        const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
-                        rel = blk == a.left_blk ? -1 : 1;
-                        vc = kk - blk * L;
-                    } else if (t >= 0 && t < L) { rel = 0; vc = t; }
-                    else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
-                    else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
-                    else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
-                    else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
-                    const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
-                    sacc += d[k] * xv;
-                    if (off == -1 && ii > 0) sub = sub + d[k];
-                    if (off == 1 && ii < 7) sup = sup + d[k];
-                }
-            }
-            const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
-            if (own) {
-                __builtin_nontemporal_store(z, a.w_out + row);
-                wbuf[tid - 8] = z;
-            }
-            __syncthreads();
-            // 3. dots of the part's rows of line x: wave wv owns items wv, wv + 7, wv + 14 (item
-            //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows
-            const double *pr = ring + slot(x) + 8;
-#pragma unroll
-            for (int u = 0; u < BAND_IT; ++u) {
-                const int itm = wv + BAND_W * u;
-                if (itm <= j) {
-                    const double *vk = VTK_BAND_REREAD ? a.V + (size_t)itm * a.ld + (int64_t)x * L + v0
-                                                       : vbuf + itm * BAND_LP;
-#pragma unroll VTK_BAND_DOTS_UNROLL
-                    for (int t = lane; t < LP; t += 64) {
-                        const double vv = vk[t];
-                        acc[u][0] += vv * pr[t];
-                        acc[u][1] += vv * wbuf[t];
-                    }
-                } else if (itm == j + 1) {
-#pragma unroll VTK_BAND_DOTS_UNROLL
-                    for (int t = lane; t < LP; t += 64) {
-                        const double pv = pr[t], wq = wbuf[t];
-                        acc[u][0] += pv * pv;
-                        acc[u][1] += pv * wq;
-                        acc[u][2] += wq * wq;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        if (it >= 1 && it <= nl) stage();   // line y is owned: its basis rows for the dots one line on
-    }
-    // per-workgroup partials in launch_dc_dots' layout for step j+1
-#pragma unroll
-    for (int u = 0; u < BAND_IT; ++u) {
-        const int itm = wv + BAND_W * u;
-        if (itm <= j + 1) {   // wave-uniform
-            const double t0 = wave_allsum(acc[u][0]), t1 = wave_allsum(acc[u][1]), t2 = wave_allsum(acc[u][2]);
-            if (lane == 0) {
-                if (itm <= j) {
-                    red[itm] = t0;
-                    red[DC_MAXJ + itm] = t1;
-                } else {
-                    red[2 * DC_MAXJ] = t0;
-                    red[2 * DC_MAXJ + 1] = t1;
-                    red[2 * DC_MAXJ + 2] = t2;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    const int jn = j + 1;
-    for (int qq = tid; qq < DC_NQ; qq += BAND_T) {
-        const bool used = qq < jn || (qq >= DC_MAXJ && qq < DC_MAXJ + jn) || qq >= 2 * DC_MAXJ;
-        if (used) a.part[(size_t)qq * GMAX + b] = red[qq];
-    }
-}
-
-static int band_geo() {
-    static const int g = [] {
-        const char *e = std::getenv("VTK_BAND_GEO");
-        const int v = e ? std::atoi(e) : VTK_BAND_GEO;
-        return v == 4 ? 4 : 2;
-    }();
-    return g;
-}
-int band_wg_per_cu() { return band_geo() == 4 ? BandGeo<4>::WPC : BandGeo<2>::WPC; }
-int band_parts(int64_t L) {
-    const int lp = band_geo() == 4 ? BandGeo<4>::LP : BandGeo<2>::LP;
-    for (int h = 1; h <= 16; ++h)
-        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= lp) return h;
-    return 0;
-}
-
-hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
-    const int geo = band_geo();
-    const int lp = geo == 4 ? BandGeo<4>::LP : BandGeo<2>::LP;
-    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > lp || (a.L / a.H_parts) % 8 != 0 ||
-        a.j + 1 > BAND_JV || grid < a.H_parts || grid > GMAX || grid % a.H_parts != 0 || grid / a.H_parts > a.X)
-        return hipErrorInvalidValue;
-    switch (a.j) {
-#define VTK_BAND_J(J_)                                                                                           \
-    case J_:                                                                                                     \
-        if (geo == 4) hipLaunchKernelGGL((k_band_step<5, J_, 4>), dim3(grid), dim3(BandGeo<4>::T), 0, s, a);    \
-        else hipLaunchKernelGGL((k_band_step<5, J_, 2>), dim3(grid), dim3(BandGeo<2>::T), 0, s, a);             \
-        break;
-        VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
-        VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
-        VTK_BAND_J(14) VTK_BAND_J(15) VTK_BAND_J(16) VTK_BAND_J(17) VTK_BAND_J(18)
-#undef VTK_BAND_J
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-// ghost exchange of the distributed band step: pack the rank's first / last line
-// of v_{j-1} (V[j-1]; V[0] at j = 0), p_j (V[j]) and w_j into send pieces of 3 L, unpack the
-// received pieces into the ghost slots (v_{j-1} -> slot j-1 when j >= 1, p_j -> m, w_j -> m+1)
-__global__ __launch_bounds__(NT) void k_ghost_pack(const double *__restrict__ V, int64_t ld, int j,
-                                                   const double *__restrict__ w, int64_t n, int L,
-                                                   double *__restrict__ sbuf, int64_t off_first, int64_t off_last) {
-    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
-        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
-        const int64_t off = side == 0 ? off_first : off_last;
-        if (off < 0) continue;
-        const int64_t row = (side == 0 ? 0 : n - L) + t;
-        const double val = vec == 0 ? V[(size_t)(j >= 1 ? j - 1 : 0) * ld + row]
-                                    : (vec == 1 ? V[(size_t)j * ld + row] : w[row]);
-        sbuf[off + r] = val;
-    }
-}
-
-__global__ __launch_bounds__(NT) void k_ghost_unpack(const double *__restrict__ rbuf, int64_t off_left, int64_t off_right,
-                                                     int j, int m, int L, double *__restrict__ ghost) {
-    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
-        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
-        const int64_t off = side == 0 ? off_left : off_right;
-        if (off < 0 || (vec == 0 && j == 0)) continue;
-        const int slot = vec == 0 ? j - 1 : m + vec - 1;
-        ghost[((size_t)side * (m + 2) + slot) * L + t] = rbuf[off + r];
-    }
-}
-
-hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,
-                             int64_t off_first, int64_t off_last, hipStream_t s) {
-    hipLaunchKernelGGL(k_ghost_pack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, V, ld, j, w, n, L, sbuf, off_first,
-                       off_last);
-    return hipGetLastError();
-}
-
-hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
-                               double *ghost, hipStream_t s) {
-    hipLaunchKernelGGL(k_ghost_unpack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, rbuf, off_left, off_right, j, m, L,
-                       ghost);
-    return hipGetLastError();
-}
-
-// distributed form of the check (local column numbering; the halo is exactly two neighbour lines,
-// halo block lblk the left one): an owned column within lines x-1..x+1 of the row's line without
-// wrap, a halo column only from the first (left block) or last (right block) local line
-__global__ __launch_bounds__(NT) void k_band_check_dist(const int32_t *__restrict__ indptr,
-                                                        const int32_t *__restrict__ indices, int64_t n, int L,
-                                                        int lblk, int *bad) {
-    const int64_t X = n / L;
-    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
-        const int64_t x = r / L, vr = r % L;
-        bool ok = true, vloc = true;
-        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
-            const int64_t c = indices[k];
-            int64_t vc;
-            if (c < 0 || c >= n + 2 * L) { ok = false; break; }
-            if (c < n) {
-                const int64_t rel = c / L - x;
-                if (rel < -1 || rel > 1) { ok = false; break; }
-                vc = c % L;
-            } else {
-                const int64_t kk = c - n, blk = kk / L;
-                if ((blk == lblk && x != 0) || (blk != lblk && x != X - 1)) { ok = false; break; }
-                vc = kk % L;
-            }
-            if (vc - vr < -1 || vc - vr > 1) vloc = false;
-        }
-        if (!ok) atomicOr(bad, 1);
-        if (!vloc) atomicOr(bad, 2);
-    }
-}
-
-hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
-                                  hipStream_t s) {
-    int64_t g = (n + NT - 1) / NT;
-    if (g > 4096) g = 4096;
-    if (g < 1) g = 1;
-    hipLaunchKernelGGL(k_band_check_dist, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, lblk, bad);
-    return hipGetLastError();
-}
-
-// *bad |= 1 when a column lies outside lines x-1..x+1 (mod X) of its row's line x; |= 2 when it
-// lies more than one row off the row's position v within its line
-__global__ __launch_bounds__(NT) void k_band_check(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
-                                                   int64_t n, int L, int X, int *bad) {
-    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
-        const int64_t x = r / L, vr = r % L;
-        bool ok = true, vloc = true;
-        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
-            const int64_t c = indices[k];
-            if (c < 0 || c >= n) { ok = false; break; }
-            int64_t rel = c / L - x;
-            if (rel > 1) rel -= X;
-            else if (rel < -1) rel += X;
-            if (rel < -1 || rel > 1) { ok = false; break; }
-            const int64_t dv = c % L - vr;
-            if (dv < -1 || dv > 1) vloc = false;
-        }
-        if (!ok) atomicOr(bad, 1);
-        if (!vloc) atomicOr(bad, 2);
-    }
-}
-
-hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
-                             hipStream_t s) {
-    int64_t g = (n + NT - 1) / NT;
-    if (g > 4096) g = 4096;
-    if (g < 1) g = 1;
-    hipLaunchKernelGGL(k_band_check, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, X, bad);
-    return hipGetLastError();
-}
 
 }  // namespace vtk

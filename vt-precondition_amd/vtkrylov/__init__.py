@@ -302,14 +302,21 @@ def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> 
         import torch
         if not (_is_device(data) and _is_device(indices) and _is_device(indptr)):
             raise TypeError("csr_matrix: data, indices and indptr must all be device tensors or all host arrays")
+        for t in (data, indices, indptr):
+            if t.device.index != ctx.device:
+                raise ValueError(f"csr_matrix: tensor on {t.device}, the context is on cuda:{ctx.device}")
         fp32 = data.dtype == torch.float32
         data = data.contiguous().to(torch.float32 if fp32 else torch.float64)
         indices = indices.contiguous().to(torch.int32)
         indptr = indptr.contiguous().to(torch.int32)
+        # the conversions above run on torch's current stream; the library copies with
+        # hipMemcpy on its own: let them finish first
+        torch.cuda.current_stream(data.device).synchronize()
+        nnz = int(indptr[-1].item())   # the CSR may carry spare capacity beyond indptr[-1]
         offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
         h = C.c_void_p()
         check(lib().vtk_csr_create(ctx.handle, int(shape[0]), None if offs is None else _np_ptr(offs),
-                                   int(indices.numel()), C.c_void_p(indptr.data_ptr()),
+                                   nnz, C.c_void_p(indptr.data_ptr()),
                                    C.c_void_p(indices.data_ptr()), C.c_void_p(data.data_ptr()),
                                    int(fp32), _abi.PTR_DEVICE, C.byref(h)), ctx.handle)
         return CsrOperator(h, ctx, fp32)
@@ -370,18 +377,19 @@ class BlockJacobi:
     applies the bs x bs diagonal-block inverses).  ``vtk_bjacobi_create``.
 
     ``mode``: how M^-1 is applied (same operator either way): "inverse" multiplies by the
-    block inverses (bit-identical to the oracle), "tridiag" solves with the LU factors of
+    block inverses (bit-identical to the oracle with setup "exact"), "tridiag" solves with the LU factors of
     tridiagonal blocks (bs 2/4/8; 24 B/row instead of 8*bs), "auto" (default) takes "tridiag"
     when every block is tridiagonal and its factors pass the setup check.
 
-    ``setup``: how the inverses are computed: "exact" (Gauss-Jordan with partial pivoting,
-    bit-identical to the oracle), "mfma" (bs 16 / 32: blocked Gauss-Jordan with the rank-4 panel
-    updates on the fp64 matrix cores; same pivot rule, rounding-level differences) or "auto"
-    (default: "mfma" for bs 16 and 32, 2.3x / 4.7x faster at C3, else "exact")."""
+    ``setup``: how the inverses are computed: "exact" (default, as ``vtk_bjacobi_create``:
+    Gauss-Jordan with partial pivoting, bit-identical to the oracle), "mfma" (bs 16 / 32: blocked
+    Gauss-Jordan with the rank-4 panel updates on the fp64 matrix cores; same pivot rule,
+    rounding-level differences) or "auto" ("mfma" for bs 16 and 32, 2.3x / 4.7x faster at C3,
+    else "exact")."""
 
     SETUPS = {"exact": 0, "mfma": 1, "auto": 2}
 
-    def __init__(self, A: CsrOperator, bs: int = 8, mode: str = "auto", setup: str = "auto"):
+    def __init__(self, A: CsrOperator, bs: int = 8, mode: str = "auto", setup: str = "exact"):
         if mode not in BJ_MODES:
             raise ValueError(f"mode must be one of {sorted(BJ_MODES)}")
         if setup not in self.SETUPS:
@@ -450,7 +458,7 @@ class BlockJacobi:
             pass
 
 
-def block_jacobi(A: CsrOperator, bs: int = 8, mode: str = "auto", setup: str = "auto") -> BlockJacobi:
+def block_jacobi(A: CsrOperator, bs: int = 8, mode: str = "auto", setup: str = "exact") -> BlockJacobi:
     return BlockJacobi(A, bs, mode, setup)
 
 

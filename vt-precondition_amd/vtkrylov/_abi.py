@@ -61,6 +61,7 @@ PROTOTYPES = {
     "vtk_rhs_splitmix": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, P]),
     "vtk_partition_rows": (C.c_int, [C.c_int64, P, C.c_int, C.c_int, P]),
     "vtk_halo_plan": (C.c_int, [C.c_int64, P, C.c_int, C.c_int, C.c_int64, P, P, I64P, P, P]),
+    "vtk_line_band_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_void_p]),
     "vtk_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "vtk_ctx_create": (C.c_int, [C.c_int, C.POINTER(P)]),
     "vtk_ctx_destroy": (None, [P]),
@@ -105,6 +106,14 @@ PROTOTYPES = {
 }
 
 
+ABI_VERSION = 3   # include/vtkrylov.h VTK_ABI_VERSION
+
+
+class BandGeometry(C.Structure):
+    _fields_ = [("parts", C.c_int), ("wg_per_range", C.c_int), ("waves_per_wg", C.c_int),
+                ("ranges", C.c_int), ("lines", C.c_int64)]
+
+
 class LayoutInfo(C.Structure):
     _fields_ = [("layout", C.c_int), ("matrix_bytes", C.c_double), ("sell_chunks", C.c_int64),
                 ("sell_entries", C.c_int64), ("wide_chunks", C.c_int64)]
@@ -142,7 +151,7 @@ def lib() -> C.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.vtk_abi_version() != 2:
+        if L.vtk_abi_version() != ABI_VERSION:
             raise ImportError("libvtkrylov.so ABI version mismatch")
         _lib = L
     return _lib
