@@ -171,21 +171,22 @@ def _band_plan(vk_lib, n, L, ncu=256):
 
 def test_line_band_plan_geometry(vk_lib):
     """The band step's geometry (vtk_line_band_plan, ABI 3): C3 = 25 000 lines of 800 rows ->
-    15 parts of <= 56 rows in two 8-wave workgroups per range, one workgroup per CU."""
+    two 400-row parts per line, one 7-wave workgroup per part, two workgroups per CU."""
     st, g = _band_plan(vk_lib, 20_000_000, 800)
     assert st == vk_lib._abi.OK
-    assert (g.parts, g.wg_per_range, g.waves_per_wg, g.ranges, g.lines) == (15, 2, 8, 128, 25_000)
-    st, g = _band_plan(vk_lib, 64 * 32, 32)   # S2: one part per line, one-wave workgroups
-    assert st == vk_lib._abi.OK and (g.parts, g.wg_per_range, g.waves_per_wg, g.ranges) == (1, 1, 1, 32)
-    st, g = _band_plan(vk_lib, 24 * 1000, 1000)   # 125 blocks: 18 parts, 3 workgroups of 6 waves
-    assert st == vk_lib._abi.OK and g.parts == 18 and g.wg_per_range * g.waves_per_wg >= 18 and g.waves_per_wg <= 8
-    assert g.ranges == 12   # X / 2
+    assert (g.parts, g.wg_per_range, g.waves_per_wg, g.ranges, g.lines) == (2, 2, 7, 256, 25_000)
+    st, g = _band_plan(vk_lib, 64 * 32, 32)   # S2: one part per line; 32 ranges of 2 lines
+    assert st == vk_lib._abi.OK and (g.parts, g.ranges) == (1, 32)
+    st, g = _band_plan(vk_lib, 24 * 1000, 1000)   # five 200-row parts; X / 2 = 12 ranges
+    assert st == vk_lib._abi.OK and (g.parts, g.ranges) == (5, 12)
 
 
-@pytest.mark.parametrize("n,L", [(2**31, 1024), (2**30 + 2**20, 1024), (800 * 7 + 8, 800), (800, 800), (1000, 100), (0, 8)])
+@pytest.mark.parametrize("n,L", [(2**31, 1024), (2**30 + 2**20, 1024), (800 * 7 + 8, 800), (800, 800), (1000, 100),
+                                 (0, 8), (24 * 404, 404)])
 def test_line_band_plan_rejects(vk_lib, n, L):
     """32-bit index guard (slabs whose rows + halo reach 2^30), partial lines, one line, line
-    lengths not a multiple of 8: VTK_ERR_ARG with a message, no GPU needed."""
+    lengths not a multiple of 8, no equal split into 8-row-multiple parts of <= 400 rows:
+    VTK_ERR_ARG with a message, no GPU needed."""
     st, _ = _band_plan(vk_lib, n, L)
     assert st == vk_lib._abi.ERR_ARG
     assert vk_lib._abi.last_error()

@@ -49,11 +49,29 @@ CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv
 
 
 def load(path):
+    """kernel name -> [(counter value, dispatch duration us)] of one --pmc pass (the counter CSV
+    carries each dispatch's own start / end stamps)"""
     d = collections.defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
-            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            d[r["Kernel_Name"]].append((float(r["Counter_Value"]), dur))
     return d
+
+
+def working(rows):
+    """the dispatches that did the work: kernels enqueued past a cycle's stop column return at
+    entry (a few us); keep those longer than 5 % of the class's longest dispatch"""
+    if not rows:
+        return rows
+    cut = 0.05 * max(d for _, d in rows)
+    return [(v, d) for v, d in rows if d > cut]
+
+
+def band_j(name):
+    """step index J of a band-step instantiation (k_band_step<WU, J, GEO>)"""
+    m = re.match(r"void vtk::k_band_step<\d+, (\d+),", name)
+    return int(m.group(1)) if m else None
 
 
 def trace_durations(path):
@@ -101,12 +119,14 @@ def main():
     out = {"_how": ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                     f"'{a.cmd}'; "
                     "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
-                    "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)"),
+                    "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM), averaged over the "
+                    "working dispatches (longer than 5 % of the class's longest; early-exit launches past a "
+                    "cycle's stop column excluded); band_step_per_j: the same per step index J"),
            "note": a.note, "config": a.config, "kernels_sha16": ksha, "kernels": {}, "durations_us": {}}
     for cls, prefix in CLASSES.items():
         rx = re.compile(prefix if prefix.startswith("void") else re.escape(prefix))
-        fk = [v for k, vs in fetch.items() if rx.match(k) for v in vs]
-        wk = [v for k, vs in write.items() if rx.match(k) for v in vs]
+        fk = [t for k, vs in fetch.items() if rx.match(k) for t in vs]
+        wk = [t for k, vs in write.items() if rx.match(k) for t in vs]
         dur = [v for k, vs in durations.items() if rx.match(k) for v in vs]
         if dur:
             # kernels enqueued past a cycle's stop column return at entry (a few us); the
@@ -118,9 +138,30 @@ def main():
                                         "early_exit": len(dur) - len(act)}
         if not fk:
             continue
-        f_kib, w_kib = statistics.mean(fk), statistics.mean(wk) if wk else 0.0
-        out["kernels"][cls] = {"dispatches": len(fk), "fetch_kib": f_kib, "write_kib": w_kib,
-                               "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024}
+        # averaged over the WORKING dispatches only (early-exit launches past a cycle's stop
+        # column would dilute the per-launch traffic)
+        fw, ww = working(fk), working(wk)
+        f_kib = statistics.mean(v for v, _ in fw)
+        w_kib = statistics.mean(v for v, _ in ww) if ww else 0.0
+        out["kernels"][cls] = {"dispatches": len(fk), "working_dispatches": len(fw), "fetch_kib": f_kib,
+                               "write_kib": w_kib, "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024}
+        if cls == "band_step":   # per step index J (the kernel is instantiated per J)
+            perj = {}
+            for k, vs in fetch.items():
+                jj = band_j(k)
+                if jj is not None and rx.match(k):
+                    perj.setdefault(jj, [[], []])[0].extend(working(vs))
+            for k, vs in write.items():
+                jj = band_j(k)
+                if jj is not None and rx.match(k):
+                    perj.setdefault(jj, [[], []])[1].extend(working(vs))
+            out["band_step_per_j"] = {
+                str(jj): {"working_dispatches": len(f), "fetch_kib": statistics.mean(v for v, _ in f),
+                          "write_kib": statistics.mean(v for v, _ in w) if w else 0.0,
+                          "hbm_bytes_per_launch": (2 * statistics.mean(v for v, _ in f) +
+                                                   (statistics.mean(v for v, _ in w) if w else 0.0)) * 1024,
+                          "mean_duration_us_profiled": statistics.mean(d for _, d in f)}
+                for jj, (f, w) in sorted(perj.items()) if f}
     if a.sq:
         rows = collections.defaultdict(lambda: collections.defaultdict(list))
         with open(os.path.join(src, a.sq, "run_counter_collection.csv")) as f:
@@ -154,7 +195,9 @@ def main():
             f.write(json.dumps(b) + "\n")
         print("patched", a.patch_bench)
     for k, v in out["kernels"].items():
-        print(f"  {k:12s} {v['dispatches']:6d} dispatches  {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch")
+        print(f"  {k:12s} {v['working_dispatches']:6d} working dispatches  {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch")
+    for jj, v in out.get("band_step_per_j", {}).items():
+        print(f"  band j={jj:>2s} {v['working_dispatches']:4d} working  {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch")
     for k, v in out["durations_us"].items():
         print(f"  {k:12s} {v['working']:4d} working launches {v['mean_working']:9.1f} us "
               f"(all {v['dispatches']}: {v['mean_all']:.1f} us)")

@@ -335,6 +335,9 @@ SpmvIn split_in(vtk_csr *A, vtk_prec *M, const double *x, bool interior) {
 int setup_halo(vtk_csr *A) {
     vtk_ctx *c = A->ctx;
     const int W = c->world;
+    // the indices may still be in flight on the context's (non-blocking) stream (device
+    // assembly): hipMemcpy on the null stream does not wait for it
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     std::vector<int32_t> idx((size_t)A->nnz);
     if (A->nnz) HIPCHK(c, hipMemcpy(idx.data(), A->d_indices, A->nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
     int64_t nh = 0;
@@ -714,6 +717,11 @@ int band_check_all(vtk_csr *A, int64_t L) {
     vtk_ctx *c = A->ctx;
     BandCheck chk;
     int rc = band_check(A, L, chk);
+    static const bool dbg = [] { const char *e = std::getenv("VTK_DEBUG_BAND"); return e && e[0] == '1'; }();
+    if (dbg)
+        std::fprintf(stderr, "[vtk band] rank %d/%d L=%lld n_local=%lld n_halo=%lld n_send=%lld local rc=%d vloc=%d ghost=%d\n",
+                     c->rank, c->world, (long long)L, (long long)A->n_local, (long long)A->n_halo, (long long)A->n_send, rc,
+                     (int)chk.vloc, (int)chk.ghost);
     if (c->dist) {
         double mine = rc == VTK_OK ? 0.0 : 1.0, bad = 0.0;
         HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -763,8 +771,7 @@ struct Solver {
     // line-band DCGS2 step (k_band_step): grid, w double buffer (s.w / s.tmp by step parity),
     // first/last-line copies of p per workgroup (two sets, by step parity)
     bool band = false;
-    bool band_wave = true;                   // k_band_wave (default) or k_band_step (VTK_BAND_IMPL=wg)
-    int band_G = 0, band_H = 1, band_gp = 1, band_hw = 1;
+    int band_G = 0, band_H = 1;
     double *edge[2] = {nullptr, nullptr};
     double *vedge[2] = {nullptr, nullptr};   // per-line part-boundary rows of p (band_H > 1)
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
@@ -970,9 +977,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.H_parts = s.band_H;
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
-            a.gp = s.band_gp;
-            if (s.band_wave) HIPCHK(c, launch_band_wave(a, s.band_G, s.band_hw, s.A->sell.uniform_w, c->stream));
-            else HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
+            HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
             HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
@@ -1025,39 +1030,16 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
              A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
              M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_fused(M) && bj_op(M).tri != nullptr && m >= 2 && m <= 20;
     int band_R = 0;
-    static const bool band_wave_env = [] { const char *e = std::getenv("VTK_BAND_IMPL"); return !(e && std::strcmp(e, "wg") == 0); }();
-    s.band_wave = band_wave_env;
     if (s.band) {
-        const int64_t X = n / A->band_L;
-        const int64_t ncu = c->n_cu > 0 ? c->n_cu : 256;
-        if (s.band_wave) {
-            // wave-independent step: parts of <= 56 rows (> 1 part needs the v-locality of the
-            // couplings), gp workgroups of <= 8 waves per line range, as many workgroups as fit
-            // at 2 waves/SIMD (8 waves per CU: L = 800 -> 128 ranges of two workgroups), >= 2
-            // lines per range.  The geometry is the same for every step of the cycle (the edge
-            // copies one step writes are indexed by the ranges of the next).
-            vtk_band_geometry g{};
-            if (vtk_line_band_plan(n, A->band_L, (int)ncu, &g) != VTK_OK || (g.parts > 1 && !A->band_vloc)) {
-                s.band = false;
-            } else {
-                band_R = g.ranges;
-                s.band_H = g.parts;
-                s.band_gp = g.wg_per_range;
-                s.band_hw = g.waves_per_wg;
-                s.band_G = band_R * g.wg_per_range;
-                if (band_R < 1) s.band = false;
-            }
+        // parts per line (rows per workgroup <= 400; > 1 needs the v-locality of the couplings),
+        // two workgroups per CU, >= 2 lines per range (vtk_line_band_plan)
+        vtk_band_geometry g{};
+        if (vtk_line_band_plan(n, A->band_L, c->n_cu, &g) != VTK_OK || (g.parts > 1 && !A->band_vloc)) {
+            s.band = false;
         } else {
-            // round-2 workgroup step: parts per line (rows per workgroup <= 400; > 1 needs the
-            // v-locality of the couplings), two workgroups per CU, >= 2 lines per range
-            s.band_H = band_parts(A->band_L);
-            if (s.band_H < 1 || (s.band_H > 1 && !A->band_vloc)) s.band = false;
-            else {
-                const int64_t wg = (int64_t)band_wg_per_cu() * ncu;
-                band_R = (int)std::min<int64_t>({wg / s.band_H, X / 2, (int64_t)GMAX / s.band_H});
-                s.band_G = band_R * s.band_H;
-                if (band_R < 1) s.band = false;
-            }
+            band_R = g.ranges;
+            s.band_H = g.parts;
+            s.band_G = band_R * g.parts;
         }
     }
     // every rank takes the same path: the band step exchanges ghost lines with its neighbours
@@ -1484,6 +1466,9 @@ int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t
     if (nnz) {
         HIPCHK(c, hipMemcpy(A->d_indices, indices, nnz * sizeof(int32_t), kd));
         HIPCHK(c, hipMemcpy(A->d_data, data, nnz * vb, kd));
+        // device-to-device copies on the null stream: complete before the context's
+        // (non-blocking) stream reads the arrays
+        if (kind == VTK_PTR_DEVICE) HIPCHK(c, hipStreamSynchronize(nullptr));
     }
     if (kind == VTK_PTR_DEVICE && nnz) {   // device input: the same range check on the device
         DBuf mmb;

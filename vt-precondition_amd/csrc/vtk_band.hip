@@ -31,13 +31,15 @@ namespace vtk {
 // ------------------------------------------------------------------------------------------
 constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
 // geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
-// 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU)
+// 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU); the host plans with the GEO 2
+// constants (vtk_internal.hpp BAND_LP / BAND_T / BAND_WPC, vtk_line_band_plan)
 template <int GEO> struct BandGeo;
-template <> struct BandGeo<2> { static constexpr int LP = 400, T = 448, WPC = 2; };
+template <> struct BandGeo<2> { static constexpr int LP = BAND_LP, T = BAND_T, WPC = BAND_WPC; };
 template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4; };
 #ifndef VTK_BAND_GEO
 #define VTK_BAND_GEO 2
 #endif
+static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 2 constants");
 #ifndef VTK_BAND_DOTS_UNROLL
 #define VTK_BAND_DOTS_UNROLL 2   // the dots' 64-row passes issued together (LDS latency once per group)
 #endif
@@ -300,14 +302,6 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     }
 }
 
-int band_wg_per_cu() { return BandGeo<VTK_BAND_GEO>::WPC; }
-int band_parts(int64_t L) {
-    const int lp = BandGeo<VTK_BAND_GEO>::LP;
-    for (int h = 1; h <= 16; ++h)
-        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= lp) return h;
-    return 0;
-}
-
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     constexpr int lp = BandGeo<VTK_BAND_GEO>::LP;
     if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > lp || (a.L / a.H_parts) % 8 != 0 ||
@@ -318,267 +312,6 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
         hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
-        break;
-        VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
-        VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
-        VTK_BAND_J(14) VTK_BAND_J(15) VTK_BAND_J(16) VTK_BAND_J(17) VTK_BAND_J(18)
-#undef VTK_BAND_J
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------
-// Line-band DCGS2 step, wave-independent form (round 3, the default).  The same
-// sweep and the same arithmetic as k_band_step, cut differently:
-//  * a WAVEFRONT owns rows [v0, v0 + nrow) of the lines [xa, xb) of its line range (nrow <= 56:
-//    whole 8-row BJ blocks on lanes 0..nrow-1) and walks them with no workgroup barrier: lane
-//    nrow recomputes the v-halo row v0 + nrow and lane 63 the row v0 - 1 (p_j from the
-//    neighbour part's boundary copies, as before), so every SpMV gather of the part's rows
-//    comes from a per-wave LDS ring of 4 lines that the same wavefront writes (in-order LDS);
-//  * the dots are row-owned: a lane accumulates s = V^T p_{j+1} and |p|^2 for its row while it
-//    updates the line (V_k, v_j and p_{j+1} are in its registers then), keeps the line's V_k,
-//    v_j and p in registers across the next line's update and SpMV, and accumulates z = V^T w,
-//    p.w, |w|^2 once w of the line is known.  No dot operand goes through LDS, and the one
-//    workgroup barrier is the final reduction (per-wave DPP sums, then the waves in order);
-//  * a workgroup holds up to 8 parts of one line range (L = 800: 15 parts, two workgroups of 8
-//    and 7 waves), so most halo rows a wave recomputes were just read by its neighbour part on
-//    the same CU; the row-owned dots need 4 (j+1) doubles per lane (two waves per SIMD: <= 256
-//    VGPRs, one 8-wave workgroup per CU).
-// v_j, p_{j+1} and w are bit-identical to k_dc_update / k_sell (same operations, same order);
-// the dots are summed in another fixed order (deterministic).
-// ------------------------------------------------------------------------------------------
-constexpr int BW_MAXW = BAND_WAVE_MAXW;   // wavefronts per workgroup (2 per SIMD)
-
-template <int J>
-__global__ __launch_bounds__(BW_MAXW * 64) void k_band_wave(BandK a) {
-    constexpr int j = J;
-    constexpr int WU = 5;
-    __shared__ double ring_all[BW_MAXW * 4 * 64];
-    __shared__ double red[BW_MAXW * DC_NQ];
-    __shared__ double cs[BAND_JV], ce[BAND_JV];
-    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
-        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m);
-        return;
-    }
-    if (stopped(&a.st->stop_col, j)) return;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, HW = (int)blockDim.x >> 6;
-    const int L = a.L, X = a.X, H = a.H_parts, GP = a.gp;
-    const int R = (int)gridDim.x / GP, rb = (int)blockIdx.x / GP;
-    const int h = ((int)blockIdx.x % GP) * HW + wv;   // the wave's part of the line
-    const bool wact = h < H;
-    const int NB = L >> 3;
-    const int blk0 = wact ? (int)((int64_t)h * NB / H) : 0, blk1 = wact ? (int)((int64_t)(h + 1) * NB / H) : 0;
-    const int v0 = 8 * blk0, nrow = 8 * (blk1 - blk0);
-    const bool own = wact && lane < nrow;
-    const bool rh = wact && lane == nrow && v0 + nrow < L;   // v-halo row after the part
-    const bool lh = wact && lane == 63 && v0 > 0;            // v-halo row before it
-    const bool upd = own || rh || lh;
-    const int v = own ? v0 + lane : (rh ? v0 + nrow : (lh ? v0 - 1 : v0));
-    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
-    const int nl = xb - xa;
-    const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
-    const int ii = lane & 7;
-    double *ring = ring_all + wv * 256;
-    for (int k = tid; k < j; k += (int)blockDim.x) {
-        cs[k] = a.cf->s[k];
-        ce[k] = a.cf->e[k];
-    }
-    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j];
-    __syncthreads();
-    // row-owned dot accumulators of step j+1: S[k] = V_k . p_{j+1}, Z[k] = V_k . w (k <= j, V_j = v_j)
-    double S[J + 1], Z[J + 1];
-    double aa = 0.0, ab = 0.0, ag = 0.0;
-#pragma unroll
-    for (int k = 0; k <= J; ++k) S[k] = Z[k] = 0.0;
-    double Vx[J + 1];   // V_k (k < j) and v_j of the previous line on the lane's row
-    double px = 0.0;    // p_{j+1} of the previous line on the lane's row
-#pragma unroll
-    for (int k = 0; k <= J; ++k) Vx[k] = 0.0;
-    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1)
-    auto line_of = [&](int it, int &kind) {
-        kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
-        return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
-    };
-    struct Ld {
-        double v[J > 0 ? J : 1];
-        double pj, wj;
-    };
-    // update operands of iteration it's line on the lane's row: V_k (k < j), p_j, w_j.  x-halo
-    // lines: p_j from the owner range's edge copy, or the ghost buffer across ranks; owned
-    // lines' v-halo rows: p_j from the neighbour part's boundary copy (the owners overwrite p_j
-    // in place with v_j)
-    auto load = [&](int it, Ld &o) {
-        int kind;
-        const int y = line_of(it, kind);
-        const int64_t row = (int64_t)y * L + v;
-        o.pj = 0.0;
-        o.wj = 0.0;
-        const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
-                               ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
-        if (upd) {
-            if (gh) {
-                o.pj = gh[(size_t)a.m * L + v];
-                o.wj = gh[(size_t)(a.m + 1) * L + v];
-            } else {
-                if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
-                else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
-                else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
-                else o.pj = a.vedge_in[((size_t)y * H + (lh ? h - 1 : h + 1)) * 2 + (lh ? 1 : 0)];
-                o.wj = __builtin_nontemporal_load(a.w_in + row);
-            }
-        }
-        if (gh) {
-#pragma unroll
-            for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
-        } else {
-#pragma unroll
-            for (int k = 0; k < J; ++k) o.v[k] = upd ? __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row) : 0.0;
-        }
-    };
-    if (wact) {
-        for (int it = 0; it <= nl + 1; ++it) {
-            const int y = xa - 1 + it, x = y - 1;
-            const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
-            // the SpMV operands of line x (independent of the update): codes, dictionary, values, m
-            const int64_t lrow = (int64_t)(work ? x : xa) * L;
-            const int64_t row = lrow + v;
-            const int64_t q = row >> 6, q0 = (lrow + v0) >> 6;
-            const int l64 = (int)(row & 63);
-            uint32_t word = 0u;
-            int dv = 0;
-            double d[WU];
-            double mrow = 1.0;
-#pragma unroll
-            for (int k = 0; k < WU; ++k) d[k] = 0.0;
-            if (work) {
-                const int64_t qd = q0 + (lane >> 4);
-                dv = (lane < 32 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
-                if (own) {
-                    word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
-#pragma unroll
-                    for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
-                    mrow = __builtin_nontemporal_load(a.mtri + row);
-                }
-            }
-            // 1. update of line y (k_dc_update's operations); stores on owned lines
-            int kind;
-            const int yl = line_of(it, kind);
-            Ld cu;
-            load(it, cu);
-            const int64_t urow = (int64_t)yl * L + v;
-            double av = cu.pj, tv = cu.wj;
-#pragma unroll
-            for (int k = 0; k < J; ++k) {
-                const double sk = cs[k], ek = ce[k];
-                av = av - sk * cu.v[k];
-                tv = tv - ek * cu.v[k];
-            }
-            double vj = cu.pj;
-            if (j >= 1) vj = av * rinv;
-            tv = tv - ej * vj;
-            const double pn = tv * qc;
-            if (kind == 0 && own) {
-                if (j >= 1) __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + urow);
-                __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + urow);
-                if (yl == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
-                if (yl == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
-                if (H > 1 && lane == 0) a.vedge_out[((size_t)yl * H + h) * 2] = pn;
-                if (H > 1 && lane == nrow - 1) a.vedge_out[((size_t)yl * H + h) * 2 + 1] = pn;
-                // s = V_{j+1}^T p_{j+1} and |p|^2 on the lane's row of line y
-#pragma unroll
-                for (int k = 0; k < J; ++k) S[k] += cu.v[k] * pn;
-                S[J] += vj * pn;
-                aa += pn * pn;
-            }
-            if (upd) ring[(it & 3) * 64 + lane] = pn;
-            __builtin_amdgcn_wave_barrier();   // the wave's own LDS writes precede its reads (in-order LDS)
-            if (work) {
-                // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
-                double sacc = 0.0, sub = 0.0, sup = 0.0;
-                const int sel = (int)(q - q0) * 16;
-#pragma unroll
-                for (int k = 0; k < WU; ++k) {
-                    const int code = (int)((word >> (4 * k)) & 15u);
-                    const int off = __shfl(dv, (sel + code) & 63, 64);
-                    if (own && code != PK_CODES) {
-                        // the column's line relative to x and its position in that line, by range
-                        // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
-                        const int t = v + off;
-                        int rel, vc;
-                        const int c = x * L + t;
-                        if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
-                            const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
-                            rel = blk == a.left_blk ? -1 : 1;
-                            vc = kk - blk * L;
-                        } else if (t >= 0 && t < L) { rel = 0; vc = t; }
-                        else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
-                        else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
-                        else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
-                        else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
-                        const int sl = vc == v0 - 1 ? 63 : vc - v0;
-                        const double xv = ring[((x - xa + 1 + rel) & 3) * 64 + sl];
-                        sacc += d[k] * xv;
-                        if (off == -1 && ii > 0) sub = sub + d[k];
-                        if (off == 1 && ii < 7) sup = sup + d[k];
-                    }
-                }
-                const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
-                if (own) {
-                    __builtin_nontemporal_store(z, a.w_out + row);
-                    // 3. z = V_{j+1}^T w, p.w, |w|^2 on the lane's row of line x
-#pragma unroll
-                    for (int k = 0; k <= J; ++k) Z[k] += Vx[k] * z;
-                    ab += px * z;
-                    ag += z * z;
-                }
-            }
-            // line y's operands for its dots one line on
-#pragma unroll
-            for (int k = 0; k < J; ++k) Vx[k] = cu.v[k];
-            Vx[J] = vj;
-            px = pn;
-        }
-    }
-    // per-wave sums (fixed DPP tree), then the workgroup's waves in order: partials of step j+1
-    // in launch_dc_dots' layout
-    double *rw = red + wv * DC_NQ;
-#pragma unroll
-    for (int k = 0; k <= J; ++k) {
-        const double ts = wave_allsum(S[k]), tz = wave_allsum(Z[k]);
-        if (lane == 0) {
-            rw[k] = ts;
-            rw[DC_MAXJ + k] = tz;
-        }
-    }
-    {
-        const double t0 = wave_allsum(aa), t1 = wave_allsum(ab), t2 = wave_allsum(ag);
-        if (lane == 0) {
-            rw[2 * DC_MAXJ] = t0;
-            rw[2 * DC_MAXJ + 1] = t1;
-            rw[2 * DC_MAXJ + 2] = t2;
-        }
-    }
-    __syncthreads();
-    const int jn = j + 1;
-    for (int qq = tid; qq < DC_NQ; qq += (int)blockDim.x) {
-        const bool used = qq < jn || (qq >= DC_MAXJ && qq < DC_MAXJ + jn) || qq >= 2 * DC_MAXJ;
-        if (!used) continue;
-        double t = 0.0;
-        for (int w = 0; w < HW; ++w) t += red[w * DC_NQ + qq];
-        a.part[(size_t)qq * GMAX + blockIdx.x] = t;
-    }
-}
-
-hipError_t launch_band_wave(const BandK &a, int grid, int hw, int wu, hipStream_t s) {
-    if (wu != 5 || a.L % 8 != 0 || a.H_parts < 1 || a.gp < 1 || hw < 1 || hw > BW_MAXW || a.gp * hw < a.H_parts ||
-        a.j + 1 > BAND_JV || grid < a.gp || grid > GMAX || grid % a.gp != 0 || grid / a.gp > a.X / 2 ||
-        a.n > INT32_MAX / 2 || (int64_t)a.X * a.L != a.n)
-        return hipErrorInvalidValue;
-    switch (a.j) {
-#define VTK_BAND_J(J_)                                                                       \
-    case J_:                                                                                 \
-        hipLaunchKernelGGL((k_band_wave<J_>), dim3(grid), dim3(64 * hw), 0, s, a);           \
         break;
         VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
         VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)

@@ -73,19 +73,12 @@ bool vlasov_params_ok(const vtk_vlasov_params *p) { return valid_params(p); }
 using namespace vtk;
 
 namespace vtk {
-// geometry of the wave-independent band step for lines of L rows (L % 8 == 0): H parts of
-// <= 56 rows (whole 8-row blocks, sizes differing by at most one block), gp workgroups of hw
-// wavefronts per line range; false when L is not a multiple of 8
-bool band_wave_plan(int64_t L, int *H, int *gp, int *hw) {
-    if (L <= 0 || L % 8 != 0) return false;
-    const int64_t nb = L / 8;
-    const int64_t h = (nb + BAND_WAVE_ROWS / 8 - 1) / (BAND_WAVE_ROWS / 8);
-    const int64_t g = (h + BAND_WAVE_MAXW - 1) / BAND_WAVE_MAXW;
-    if (h > INT32_MAX / 64) return false;
-    *H = (int)h;
-    *gp = (int)g;
-    *hw = (int)((h + g - 1) / g);
-    return true;
+// parts of a line of L rows for the band step: the fewest equal parts of <= BAND_LP rows, each
+// a multiple of 8 rows (whole BJ blocks); 0 when there is none
+int band_parts(int64_t L) {
+    for (int h = 1; h <= 16; ++h)
+        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= BAND_LP) return h;
+    return 0;
 }
 
 }  // namespace vtk
@@ -230,22 +223,24 @@ int vtk_line_band_plan(int64_t n_local, int64_t line_len, int n_cu, vtk_band_geo
         return VTK_ERR_ARG;
     }
     const int64_t X = n_local / line_len;
-    // k_band_wave indexes rows, and columns of the two halo lines, in 32-bit integers
+    // the band kernels index rows, and columns of the two halo lines, in 32-bit integers
     if (X < 2 || n_local + 2 * line_len >= INT32_MAX / 2) {
         set_context_free_error("vtk_line_band_plan: fewer than 2 lines, or the slab exceeds 32-bit indices");
         return VTK_ERR_ARG;
     }
-    int H = 0, gp = 0, hw = 0;
-    if (!vtk::band_wave_plan(line_len, &H, &gp, &hw)) {
-        set_context_free_error("vtk_line_band_plan: line_len must be a multiple of 8");
+    const int H = vtk::band_parts(line_len);
+    if (H < 1) {
+        set_context_free_error("vtk_line_band_plan: no split of the line into equal parts of <= 400 rows, "
+                               "each a multiple of 8");
         return VTK_ERR_ARG;
     }
     const int64_t ncu = n_cu > 0 ? n_cu : 256;
-    const int64_t wpc = std::max(1, 8 / hw);   // 8-wave workgroups: one per CU (two waves per SIMD)
-    const int64_t R = std::min<int64_t>({std::max<int64_t>(1, wpc * ncu / gp), X / 2, (int64_t)vtk::GMAX / gp});
+    // BAND_WPC workgroups per CU; >= 2 lines per range; the partial slots bound the grid
+    const int64_t R = std::min<int64_t>({std::max<int64_t>(1, (int64_t)vtk::BAND_WPC * ncu / H), X / 2,
+                                         (int64_t)vtk::GMAX / H});
     out->parts = H;
-    out->wg_per_range = gp;
-    out->waves_per_wg = hw;
+    out->wg_per_range = H;
+    out->waves_per_wg = vtk::BAND_T / 64;
     out->ranges = (int)R;
     out->lines = X;
     return VTK_OK;

@@ -344,7 +344,7 @@ hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64
                             const DcCoef *cf, int grid, const GmresState *st, double *x,
                             const double *H, const double *S, int m, int nt_pw, hipStream_t s);
 
-// Line-band DCGS2 step (k_band_wave / k_band_step): update pass of step j + SpMV, tridiagonal
+// Line-band DCGS2 step (k_band_step): update pass of step j + SpMV, tridiagonal
 // BJ(8) and dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded
 // columns, fp64 values; across ranks through the ghost lines).  grid workgroups (<= X lines, <= GMAX), partials of step j+1 in
 // the launch_dc_dots layout; edge_in / edge_out: [grid][2][L] first/last-line copies of p.
@@ -372,23 +372,18 @@ struct BandK {
     const double *ghost;         // distributed: [2][m+2][L] the left / right neighbour lines'
                                  // v_k (k < j), p_j, w_j (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
-    int gp = 1;                  // k_band_wave: workgroups per line range (grid = ranges x gp)
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
-// wave-independent form (k_band_wave, the default): parts of <= 56 rows per wavefront, hw
-// wavefronts per workgroup, a.gp workgroups per line range (band_wave_plan)
-constexpr int BAND_WAVE_ROWS = 56;   // rows a wavefront owns (7 BJ blocks; lanes 56 / 63: v-halo rows)
-constexpr int BAND_WAVE_MAXW = 8;    // wavefronts per workgroup (two per SIMD: <= 256 VGPRs)
-bool band_wave_plan(int64_t L, int *H, int *gp, int *hw);   // vtk_host.cpp
-hipError_t launch_band_wave(const BandK &a, int grid, int hw, int wu, hipStream_t s);
+// geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
+// line (one part; parts per line = band_parts), BAND_WPC workgroups per CU (LDS-bound)
+constexpr int BAND_LP = 400, BAND_T = 448, BAND_WPC = 2;
 hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
                                   hipStream_t s);
 hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,
                              int64_t off_first, int64_t off_last, hipStream_t s);
 hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
                                double *ghost, hipStream_t s);
-int band_wg_per_cu();         // band step workgroups per CU
-int band_parts(int64_t L);    // parts per line (rows per part <= 400, multiple of 8); 0: none
+int band_parts(int64_t L);    // parts per line (rows per part <= BAND_LP, multiple of 8); 0: none (vtk_host.cpp)
 // *bad |= 1 when some column is outside the lines x-1..x+1 (mod X) of its row, |= 2 when one is
 // more than one row off its row's position in the line (bad zeroed by the caller)
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
