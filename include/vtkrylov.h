@@ -210,7 +210,8 @@ int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out);
  * neighbour lines as its halo, and the band is set on every rank or on none.  With it,
  * vtk_gmres runs each DCGS2 update pass together with the next step's SpMV + BJ + dots in one
  * sweep (SELL layout, tridiagonal BJ(8), restart <= 20; across ranks the neighbours' edge lines
- * travel as ghost lines each step): the basis is read once per Arnoldi step instead of twice.
+ * of v_{j-1} and w_j travel as ghost lines each step): the basis is read once per Arnoldi step
+ * instead of twice, and the candidate p_j is recomputed in registers instead of stored.
  * Same operator, same update arithmetic. */
 int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len);
 int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len);

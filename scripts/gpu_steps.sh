@@ -74,6 +74,7 @@ for s in "$@"; do
         mr4dbg) VTK_DEBUG_BAND=1 step mr4dbg 300 python -u -m pytest tests/test_gpu_multirank.py -x -v -s -k "S2-4" -p no:cacheprovider --timeout 200 --timeout-method thread ;;
         mrlarge) step mrlarge 900 python -u -m pytest tests/test_gpu_multirank_large.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
         sqband) for impl in wg wave; do VTK_BAND_IMPL=$impl step sqband_$impl 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT -d gpurun_out/sqband_$impl -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 2 || exit $?; done ;;
+        bandtests) step bandtests 600 python -u -m pytest tests/test_gpu_band.py tests/test_gpu_multirank.py tests/test_gpu_large.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
         testsv) step testsv 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         large) step large 600 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         *) echo "unknown step $s"; exit 2 ;;

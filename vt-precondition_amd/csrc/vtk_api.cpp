@@ -670,10 +670,10 @@ int band_check_dist(vtk_csr *A, int64_t L, bool &solo, BandLayout &out) {
     for (int q = 0; q < W; ++q) {
         out.soff[q] = so;
         out.roff[q] = ro;
-        if (q == pr) { out.off_last = so; so += 3 * L; }
-        if (q == pl) { out.off_first = so; so += 3 * L; }
-        if (q == pl) { out.off_left = ro; ro += 3 * L; }
-        if (q == pr) { out.off_right = ro; ro += 3 * L; }
+        if (q == pr) { out.off_last = so; so += BAND_GHOST_VECS * L; }
+        if (q == pl) { out.off_first = so; so += BAND_GHOST_VECS * L; }
+        if (q == pl) { out.off_left = ro; ro += BAND_GHOST_VECS * L; }
+        if (q == pr) { out.off_right = ro; ro += BAND_GHOST_VECS * L; }
         out.scnt[q] = so - out.soff[q];
         out.rcnt[q] = ro - out.roff[q];
     }
@@ -768,12 +768,11 @@ struct Solver {
     double *Hraw = nullptr, *dcpart = nullptr;   // DCGS2
     DcCoef *cf = nullptr;
     double *x = nullptr;                         // the solution (the DCGS2 update pass may update it)
-    // line-band DCGS2 step (k_band_step): grid, w double buffer (s.w / s.tmp by step parity),
-    // first/last-line copies of p per workgroup (two sets, by step parity)
+    // line-band DCGS2 step (k_band_step): grid, parts per line; w rotates over s.w, s.tmp, w3
+    // (step j's w in the buffer j % 3: the band step reads w_{j-1} and w_j, writes w_{j+1})
     bool band = false;
     int band_G = 0, band_H = 1;
-    double *edge[2] = {nullptr, nullptr};
-    double *vedge[2] = {nullptr, nullptr};   // per-line part-boundary rows of p (band_H > 1)
+    double *w3 = nullptr;
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
 };
 
@@ -873,8 +872,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *pj = s.V + (size_t)j * s.ld;
         int cnt = 0;
         const double b_step = b_csr + b_inv + n8 * (j + 2);   // CSR, BJ, p, w, V_j
-        // band: step j's w and partials come from the band step j-1 (w alternates s.w / s.tmp)
-        double *w_cur = (band && (j & 1)) ? s.tmp : s.w;
+        // band: step j's w and partials come from the band step j-1 (w in buffer j % 3)
+        double *const wb[3] = {s.w, s.tmp, s.w3};
+        double *w_cur = band ? wb[j % 3] : s.w;
         if (band && j > 0) {
             cnt = s.band_G;
         } else if (fused && bj_split(s.M)) {
@@ -922,7 +922,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
         }
-        // distributed band step: the x-neighbours' edge lines of v_{j-1}, p_j, w_j travel to the
+        // distributed band step: the x-neighbours' edge lines of v_{j-1} and w_j travel to the
         // ghost buffers on the comm stream (after this step's all-reduce in RCCL order, overlapping
         // the scalar step); the band step waits for them
         const bool ghost_x = band && s.ghost && j <= m - 2;
@@ -942,14 +942,15 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         }
         if (band && j <= m - 2) {
             // update pass of step j + SpMV, BJ and dots of step j+1 in one sweep over the x-lines
-            // reads V_k (k < j), p_j, w_j; writes v_j (j >= 1: p_j is v_0 at j = 0), p_{j+1}, w_{j+1}
+            // reads V_k (k < j), w_{j-1} (v_0 at j = 0), w_j; writes v_j (j >= 1), w_{j+1} and, at
+            // j = m - 2 only, p_{j+1} (k_dc_update's operand)
             // (VTK_PROF_PERJ=1: one profile class per step index, "band_step_jNN")
             static const bool perj = [] { const char *e = std::getenv("VTK_PROF_PERJ"); return e && e[0] == '1'; }();
             static const char *const jname[] = {"band_step_j00", "band_step_j01", "band_step_j02", "band_step_j03",
                 "band_step_j04", "band_step_j05", "band_step_j06", "band_step_j07", "band_step_j08", "band_step_j09",
                 "band_step_j10", "band_step_j11", "band_step_j12", "band_step_j13", "band_step_j14", "band_step_j15",
                 "band_step_j16", "band_step_j17", "band_step_j18", "band_step_j19"};
-            Prof pf(c, perj && j < 20 ? jname[j] : "band_step", j, b_csr + b_inv + n8 * (j + (j >= 1 ? 5 : 4)));
+            Prof pf(c, perj && j < 20 ? jname[j] : "band_step", j, b_csr + b_inv + n8 * (j + (j >= 1 ? 4 : 3) + (j == m - 2 ? 1 : 0)));
             BandK a;
             a.pk = s.A->sell.d_pk;
             a.dict = s.A->sell.d_dict;
@@ -960,16 +961,13 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.j = j;
             a.m = m;
             a.w_in = w_cur;
-            a.w_out = (j & 1) ? s.w : s.tmp;
+            a.w_prev = wb[(j + 2) % 3];
+            a.w_out = wb[(j + 1) % 3];
             a.cf = s.cf;
             a.st = ds;
             a.x = s.x;
             a.H = s.H;
             a.S = s.S;
-            a.edge_in = s.edge[j & 1];
-            a.edge_out = s.edge[(j + 1) & 1];
-            a.vedge_in = s.vedge[j & 1];
-            a.vedge_out = s.vedge[(j + 1) & 1];
             a.part = s.dcpart;
             a.n = n;
             a.L = (int)s.A->band_L;
@@ -1053,11 +1051,11 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (off != 0.0) s.band = false;
     }
-    const size_t nedge1 = s.band ? (size_t)band_R * 2 * A->band_L : 0;
-    const size_t nvedge1 = s.band ? (size_t)(n / A->band_L) * s.band_H * 2 : 0;
-    const size_t nghost = (s.band && A->band_ghost) ? (size_t)2 * (m + 2) * A->band_L + 12 * (size_t)A->band_L : 0;
-    const size_t nedge = 2 * (nedge1 + nvedge1) + nghost;
-    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge + 8;
+    // band: the third w buffer, the ghost lines [2][m+2][L] and the send / receive pieces
+    const size_t nghost = (s.band && A->band_ghost)
+                              ? (size_t)2 * (m + 2) * A->band_L + 4 * (size_t)BAND_GHOST_VECS * A->band_L : 0;
+    const size_t nedge = s.band ? (size_t)s.ld + nghost : 0;
+    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge + 16;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
         c->ws = nullptr;
@@ -1082,14 +1080,12 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         HIPCHK(c, hipMemsetAsync(s.Hraw, 0, (size_t)(m + 1) * (m + 1) * sizeof(double), c->stream));
     }
     if (s.band) {
-        s.edge[0] = wp;
-        s.edge[1] = wp + nedge1;
-        s.vedge[0] = wp + 2 * nedge1;
-        s.vedge[1] = wp + 2 * nedge1 + nvedge1;
+        wp = reinterpret_cast<double *>((reinterpret_cast<uintptr_t>(wp) + 63) & ~(uintptr_t)63);
+        s.w3 = wp;
         if (A->band_ghost) {
-            s.ghost = wp + 2 * (nedge1 + nvedge1);
+            s.ghost = wp + s.ld;
             s.gsend = s.ghost + (size_t)2 * (m + 2) * A->band_L;
-            s.grecv = s.gsend + 6 * (size_t)A->band_L;
+            s.grecv = s.gsend + 2 * (size_t)BAND_GHOST_VECS * A->band_L;
         }
         wp += nedge;
     }

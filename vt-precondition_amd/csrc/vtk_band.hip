@@ -15,19 +15,22 @@ namespace vtk {
 // Vlasov operators, L = Nv -- the update pass of step j and the fused SpMV + BJ + dots of step
 // j+1 run as ONE sweep.  Workgroup (range r, part h) owns rows v0 <= v < v0 + LP (LP = L / H)
 // of the lines [xa, xb) of range r and walks them in order; at line x it
-//   1. updates line x+1 (v_j, p_{j+1} exactly as k_dc_update) on its rows plus one v-halo row
-//      on each side, and puts p_{j+1}(x+1) into an LDS ring of 4 lines,
+//   1. updates line x+1 on its rows plus one v-halo row on each side: recomputes p_j exactly as
+//      step j-1 formed it, p_j = (w_{j-1} - sum_k e'_k V_k) q' (the previous step's scalars e',
+//      q' in DcCoef::e_prev / q_prev; p_0 = v_0), then v_j and p_{j+1} as k_dc_update, and puts
+//      p_{j+1}(x+1) into an LDS ring of 4 lines,
 //   2. computes w(x) = M^-1 A p_{j+1} on its rows of line x from the ring (the SELL entries in
 //      stored order and the tridiagonal BJ solve exactly as k_sell: w is bit-identical),
 //   3. accumulates step j+1's dots s = V_{j+1}^T p_{j+1}, z = V_{j+1}^T w, |p|^2, p.w, |w|^2
 //      from LDS: the line's basis rows were staged there by step 1 one line earlier.
 // The basis is read from HBM once per step instead of twice (update pass + dots), p_{j+1} is
-// never re-read for the SpMV gathers, and one launch replaces two.  Rows another workgroup owns
-// are recomputed: the x-halo lines xa-1 and xb (their p_j from the owner's copy of its first /
-// last line from the previous step -- the owner overwrites p_j in place with v_j) and the
-// v-halo rows v0-1, v0+LP (p_j from the owner's per-line boundary copies).  7 waves; lane
-// tid <-> row v = v0 - 8 + tid (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two
-// workgroups per CU, whose update / SpMV / dots phases overlap.
+// neither stored (except by the last band step, whose successor is k_dc_update) nor re-read
+// for the SpMV gathers, and one launch replaces two.  Rows another workgroup owns are
+// recomputed from that row's own V_k, w_{j-1}, w_j: the x-halo lines xa-1 and xb and the v-halo
+// rows v0-1, v0+LP -- no per-step boundary copies between workgroups.  w cycles through three
+// buffers (w_{j-1}, w_j read, w_{j+1} written).  7 waves; lane tid <-> row v = v0 - 8 + tid
+// (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two workgroups per CU, whose update / SpMV /
+// dots phases overlap.
 // ------------------------------------------------------------------------------------------
 constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
 // geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
@@ -61,10 +64,10 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     __shared__ double ring[4 * BAND_RS];
     __shared__ double wbuf[BAND_LP];
     __shared__ double red[DC_NQ];
-    __shared__ double cs[BAND_JV], ce[BAND_JV];
+    __shared__ double cs[BAND_JV], ce[BAND_JV], cp[BAND_JV];
     constexpr int j = J;
     if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
-        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m);
+        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, a.w_prev);
         return;
     }
     if (stopped(&a.st->stop_col, j)) return;
@@ -80,49 +83,49 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     for (int k = tid; k < j; k += BAND_T) {
         cs[k] = a.cf->s[k];
         ce[k] = a.cf->e[k];
+        cp[k] = a.cf->e_prev[k];
     }
-    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j];
+    const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j], qp = a.cf->q_prev;
     __syncthreads();
     double vreg[J + 1];
     double acc[BAND_IT][3];
 #pragma unroll
     for (int u = 0; u < BAND_IT; ++u) acc[u][0] = acc[u][1] = acc[u][2] = 0.0;
-    // update of line y on the lane's row: kind 0 an owned line, 1 / 2 the x-halo line before xa /
-    // after xb-1 (p_j from the owner's edge copy; nothing stored); owned lines' v-halo rows take
-    // p_j from the neighbour part's boundary copy.  vreg = V_k(y) k < j, then v_j.
-    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1)
+    // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1;
+    // kind 1 / 2, recomputed, nothing stored)
     const int nl = xb - xa;
     auto line_of = [&](int it, int &kind) {
         kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
         return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
     };
-    // update operands of iteration it's line on the lane's row: V_k (k < j), p_j, w_j.  kind 1 / 2
-    // (x-halo lines): p_j from the owner's edge copy; owned lines' v-halo rows: p_j from the
-    // neighbour part's boundary copy (the owners overwrite p_j in place with v_j)
+    // software pipeline (J <= VTK_BAND_PF, as the registers allow): the next line's update
+    // operands are loaded during this line's SpMV and dots.  (A partial prefetch of 4 basis rows
+    // for larger J measured slower: 1234 vs 1254 it/s, spills)
+    constexpr bool PF = J <= VTK_BAND_PF;
+    // update operands of iteration it's line on the lane's row: V_k (k < j), w_{j-1} (j = 0: v_0)
+    // and w_j
     struct Ld {
         double v[J > 0 ? J : 1];
-        double pj, wj;
+        double wm, wj;
     };
     auto load = [&](int it, Ld &o) {
         int kind;
         const int y = line_of(it, kind);
         const int64_t row = (int64_t)y * L + (upd ? v : 0);
-        o.pj = 0.0;
+        o.wm = 0.0;
         o.wj = 0.0;
         // a rank's first / last line range: the x-halo line is a neighbour rank's line, whose
-        // V_k, p_j, w_j arrived in the ghost buffer (slots k, m, m + 1)
+        // V_k (k < j), w_j and w_{j-1} arrived in the ghost buffer (slots k, m + (j & 1),
+        // m + ((j - 1) & 1); v_0 in slot 0 at j = 0)
         const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
                                ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
         if (upd) {
             if (gh) {
-                o.pj = gh[(size_t)a.m * L + v];
-                o.wj = gh[(size_t)(a.m + 1) * L + v];
+                o.wj = gh[(size_t)(a.m + (j & 1)) * L + v];
+                o.wm = gh[(size_t)(j == 0 ? 0 : a.m + ((j + 1) & 1)) * L + v];
             } else {
-                if (j == 0 || (kind == 0 && own)) o.pj = __builtin_nontemporal_load(a.V + (size_t)j * a.ld + row);
-                else if (kind == 1) o.pj = a.edge_in[((size_t)((rb + R - 1) % R) * 2 + 1) * L + v];
-                else if (kind == 2) o.pj = a.edge_in[((size_t)((rb + 1) % R) * 2) * L + v];
-                else o.pj = a.vedge_in[((size_t)y * H + (tid < 8 ? h - 1 : h + 1)) * 2 + (tid < 8 ? 1 : 0)];
                 o.wj = __builtin_nontemporal_load(a.w_in + row);
+                o.wm = __builtin_nontemporal_load((j == 0 ? a.V : a.w_prev) + row);
             }
         }
         if (gh) {
@@ -135,21 +138,29 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                                                 : __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row)) : 0.0;
         }
     };
-    // the update itself (k_dc_update's operations); stores on owned lines; vreg = V_k, v_j
+    // the update itself: p_j as step j-1's update formed it, then k_dc_update's operations;
+    // stores v_j on owned lines (and p_{j+1} at the last band step); vreg = V_k, v_j
     auto update = [&](int it, const Ld &o) -> double {
         int kind;
         const int y = line_of(it, kind);
         const int64_t row = (int64_t)y * L + (upd ? v : 0);
 #pragma unroll
         for (int k = 0; k < J; ++k) vreg[k] = o.v[k];
-        double av = o.pj, tv = o.wj;
+        double pj = o.wm;   // j = 0: p_0 = v_0
+        if (j >= 1) {
+            double tp = o.wm;
+#pragma unroll
+            for (int k = 0; k < J; ++k) tp = tp - cp[k] * vreg[k];
+            pj = tp * qp;
+        }
+        double av = pj, tv = o.wj;
 #pragma unroll
         for (int k = 0; k < J; ++k) {
             const double sk = cs[k], ek = ce[k];
             av = av - sk * vreg[k];
             tv = tv - ek * vreg[k];
         }
-        double vj = o.pj;
+        double vj = pj;
         if (j >= 1) vj = av * rinv;
         tv = tv - ej * vj;
         const double pn = tv * qc;
@@ -159,11 +170,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                 if constexpr (VTK_BAND_REREAD) a.V[(size_t)j * a.ld + row] = vj;
                 else __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
             }
-            __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
-            if (y == xa) a.edge_out[((size_t)rb * 2) * L + v] = pn;
-            if (y == xb - 1) a.edge_out[((size_t)rb * 2 + 1) * L + v] = pn;
-            if (H > 1 && tid == 8) a.vedge_out[((size_t)y * H + h) * 2] = pn;
-            if (H > 1 && tid == 7 + LP) a.vedge_out[((size_t)y * H + h) * 2 + 1] = pn;
+            if (j == a.m - 2) __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
         }
         return pn;
     };
@@ -175,9 +182,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     };
     auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
     // iteration it updates line y = xa - 1 + it and, from it = 2 on, runs the SpMV and dots of
-    // line y - 1.  PF (small j, registers allow): the next line's update operands are loaded
-    // during this line's SpMV and dots (software pipeline)
-    constexpr bool PF = J <= VTK_BAND_PF;
+    // line y - 1
     Ld nx;
     if constexpr (PF) load(0, nx);
     for (int it = 0; it <= nl + 1; ++it) {
@@ -248,7 +253,9 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
             }
             __syncthreads();
             // 3. dots of the part's rows of line x: wave wv owns items wv, wv + 7, wv + 14 (item
-            //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows
+            //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows.  Items
+            //    outer: each item's loop streams one basis row against p and w (rows outer with
+            //    p, w read once per row for all items measured slower: 1268-1285 vs 1296 it/s)
             const double *pr = ring + slot(x) + 8;
 #pragma unroll
             for (int u = 0; u < BAND_IT; ++u) {
@@ -323,43 +330,44 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
 }
 
 // ghost exchange of the distributed band step: pack the rank's first / last line
-// of v_{j-1} (V[j-1]; V[0] at j = 0), p_j (V[j]) and w_j into send pieces of 3 L, unpack the
-// received pieces into the ghost slots (v_{j-1} -> slot j-1 when j >= 1, p_j -> m, w_j -> m+1)
+// of v_{j-1} (V[j-1]; V[0] at j = 0) and w_j into send pieces of BAND_GHOST_VECS L, unpack the
+// received pieces into the ghost slots (v_{j-1} -> slot j-1, v_0 -> slot 0 at j = 0, w_j ->
+// m + (j & 1): step j-1's w stays in the other slot for the recompute of p_j)
 __global__ __launch_bounds__(NT) void k_ghost_pack(const double *__restrict__ V, int64_t ld, int j,
                                                    const double *__restrict__ w, int64_t n, int L,
                                                    double *__restrict__ sbuf, int64_t off_first, int64_t off_last) {
-    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
-        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
+    constexpr int NV = BAND_GHOST_VECS;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < 2 * NV * L; i += gridDim.x * NT) {
+        const int side = i / (NV * L), r = i % (NV * L), vec = r / L, t = r % L;
         const int64_t off = side == 0 ? off_first : off_last;
         if (off < 0) continue;
         const int64_t row = (side == 0 ? 0 : n - L) + t;
-        const double val = vec == 0 ? V[(size_t)(j >= 1 ? j - 1 : 0) * ld + row]
-                                    : (vec == 1 ? V[(size_t)j * ld + row] : w[row]);
-        sbuf[off + r] = val;
+        sbuf[off + r] = vec == 0 ? V[(size_t)(j >= 1 ? j - 1 : 0) * ld + row] : w[row];
     }
 }
 
 __global__ __launch_bounds__(NT) void k_ghost_unpack(const double *__restrict__ rbuf, int64_t off_left, int64_t off_right,
                                                      int j, int m, int L, double *__restrict__ ghost) {
-    for (int i = blockIdx.x * NT + threadIdx.x; i < 6 * L; i += gridDim.x * NT) {
-        const int side = i / (3 * L), r = i % (3 * L), vec = r / L, t = r % L;
+    constexpr int NV = BAND_GHOST_VECS;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < 2 * NV * L; i += gridDim.x * NT) {
+        const int side = i / (NV * L), r = i % (NV * L), vec = r / L, t = r % L;
         const int64_t off = side == 0 ? off_left : off_right;
-        if (off < 0 || (vec == 0 && j == 0)) continue;
-        const int slot = vec == 0 ? j - 1 : m + vec - 1;
+        if (off < 0) continue;
+        const int slot = vec == 0 ? (j >= 1 ? j - 1 : 0) : m + (j & 1);
         ghost[((size_t)side * (m + 2) + slot) * L + t] = rbuf[off + r];
     }
 }
 
 hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,
                              int64_t off_first, int64_t off_last, hipStream_t s) {
-    hipLaunchKernelGGL(k_ghost_pack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, V, ld, j, w, n, L, sbuf, off_first,
+    hipLaunchKernelGGL(k_ghost_pack, dim3((2 * BAND_GHOST_VECS * L + NT - 1) / NT), dim3(NT), 0, s, V, ld, j, w, n, L, sbuf, off_first,
                        off_last);
     return hipGetLastError();
 }
 
 hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
                                double *ghost, hipStream_t s) {
-    hipLaunchKernelGGL(k_ghost_unpack, dim3((6 * L + NT - 1) / NT), dim3(NT), 0, s, rbuf, off_left, off_right, j, m, L,
+    hipLaunchKernelGGL(k_ghost_unpack, dim3((2 * BAND_GHOST_VECS * L + NT - 1) / NT), dim3(NT), 0, s, rbuf, off_left, off_right, j, m, L,
                        ghost);
     return hipGetLastError();
 }

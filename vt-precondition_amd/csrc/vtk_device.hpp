@@ -266,17 +266,23 @@ __device__ inline void hess_solve(const double *__restrict__ H, const double *__
 // it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
 static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
                                         const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
-                                        const double *__restrict__ S, int m) {
-    __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ];
-    __shared__ double rinv_s;
+                                        const double *__restrict__ S, int m, const double *__restrict__ wprev) {
+    __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ], ep[DC_MAXJ];
+    __shared__ double rinv_s, qp_s;
+    // wprev (line-band step): p_j is not stored; recompute it as step j-1 formed it
+    const bool rec = c == j && j >= 1 && wprev != nullptr;
     if (threadIdx.x == 0) {
         hess_solve(H, S, m, c, ys);
         rinv_s = cf->rinv;
+        qp_s = cf->q_prev;
     }
     if (c == j)
-        for (int k = threadIdx.x; k < j; k += blockDim.x) cs[k] = cf->s[k];
+        for (int k = threadIdx.x; k < j; k += blockDim.x) {
+            cs[k] = cf->s[k];
+            ep[k] = cf->e_prev[k];
+        }
     __syncthreads();
-    const double rinv = rinv_s;
+    const double rinv = rinv_s, qp = qp_s;
     const double *pj = V + (size_t)j * ld;
     const int kv = c == j ? j : c + 1;   // stored basis vectors in the sum
     const int64_t stride = 2 * (int64_t)gridDim.x * blockDim.x;
@@ -284,7 +290,16 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
         if (i + 1 < n) {
             double ax = 0.0, ay = 0.0;
             double2 a = make_double2(0.0, 0.0);
-            if (c == j) {
+            if (rec) {
+                const d2v wp = ldnt2(wprev + i);
+                double tx = wp.x, ty = wp.y;
+                for (int k = 0; k < j; ++k) {
+                    const d2v v = ldnt2(V + (size_t)k * ld + i);
+                    tx = tx - ep[k] * v.x;
+                    ty = ty - ep[k] * v.y;
+                }
+                a = make_double2(tx * qp, ty * qp);
+            } else if (c == j) {
                 const d2v pp = ldnt2(pj + i);
                 a = make_double2(pp.x, pp.y);
             }
@@ -309,6 +324,11 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
             st_nt2<1>(x + i, xv.x, xv.y);
         } else {
             double ax = 0.0, a = c == j ? pj[i] : 0.0;
+            if (rec) {
+                double t = wprev[i];
+                for (int k = 0; k < j; ++k) t = t - ep[k] * V[(size_t)k * ld + i];
+                a = t * qp;
+            }
             for (int k = 0; k < kv; ++k) {
                 const double v = V[(size_t)k * ld + i];
                 ax += ys[k] * v;

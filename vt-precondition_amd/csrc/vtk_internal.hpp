@@ -46,6 +46,10 @@ struct DcCoef {
     double nu;                // tentative h_{j+1,j}
     double h0[DC_MAXJ + 1];   // ||B v_c|| per column (breakdown test, iterative.py:766)
     int committed[DC_MAXJ + 1];   // column already rotated into H (early or exact commit)
+    // the previous step's e and q (k_dc_scalar saves them before overwriting): the line-band
+    // step recomputes p_j = (w_{j-1} - sum_k e_prev[k] V_k) q_prev instead of storing it
+    double e_prev[DC_MAXJ + 1];
+    double q_prev;
 };
 
 // a reduced scalar as seen by a consumer kernel: G partials (single GPU) or 1 value (after
@@ -347,7 +351,8 @@ hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64
 // Line-band DCGS2 step (k_band_step): update pass of step j + SpMV, tridiagonal
 // BJ(8) and dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded
 // columns, fp64 values; across ranks through the ghost lines).  grid workgroups (<= X lines, <= GMAX), partials of step j+1 in
-// the launch_dc_dots layout; edge_in / edge_out: [grid][2][L] first/last-line copies of p.
+// the launch_dc_dots layout.  p_j is recomputed from w_{j-1} (w_prev) and stored only for
+// j + 1 = m - 1 (k_dc_update's operand); w rotates over three buffers.
 struct BandK {
     const uint32_t *pk;
     const int32_t *dict;
@@ -356,27 +361,27 @@ struct BandK {
     double *V;
     int64_t ld;
     int j, m;
-    const double *w_in;
-    double *w_out;
+    const double *w_in;          // w_j
+    const double *w_prev;        // w_{j-1} (unused at j = 0)
+    double *w_out;               // w_{j+1}
     const DcCoef *cf;
     const GmresState *st;
     double *x;
     const double *H, *S;
-    const double *edge_in;       // [R][2][L]: first / last line of each line range (p of step j)
-    double *edge_out;
-    const double *vedge_in;      // [X][H][2]: first / last row of each line part (H > 1)
-    double *vedge_out;
     double *part;
     int64_t n;
     int L, X, H_parts;           // line length, lines, parts per line (grid = ranges x H_parts)
     const double *ghost;         // distributed: [2][m+2][L] the left / right neighbour lines'
-                                 // v_k (k < j), p_j, w_j (k_ghost_unpack); null on one rank
+                                 // v_k (k < j) and w_j, w_{j-1} by parity in slots m, m+1
+                                 // (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
 // geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
 // line (one part; parts per line = band_parts), BAND_WPC workgroups per CU (LDS-bound)
 constexpr int BAND_LP = 400, BAND_T = 448, BAND_WPC = 2;
+// vectors per ghost line and step of the distributed band step: v_{j-1} (v_0 at j = 0), w_j
+constexpr int BAND_GHOST_VECS = 2;
 hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
                                   hipStream_t s);
 hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w, int64_t n, int L, double *sbuf,

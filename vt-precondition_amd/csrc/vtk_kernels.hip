@@ -2647,6 +2647,7 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
         e_s[k] = e;
         hj[k] = h;
         Hraw[(size_t)j * M1 + k] = h;
+        cf->e_prev[k] = cf->e[k];   // the line-band step's recompute of p_j (DcCoef::e_prev)
         cf->e[k] = e;
         if (k < j) cf->s[k] = sv[k];
     }
@@ -2664,6 +2665,7 @@ __global__ __launch_bounds__(1024) void k_dc_scalar(const double *part, int cnt,
     if (!(nu > 1e-8 * gn)) nu = gn > 0.0 ? gn : 1.0;   // heavy cancellation: step j+1's r corrects
     cf->nu = nu;
     cf->h0[j] = gn;
+    cf->q_prev = cf->q;
     cf->q = 1.0 / (r * nu);
     cf->committed[j] = 0;
     if (!safe) return;
@@ -2704,7 +2706,7 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
     __shared__ double cs[DC_MAXJ], ce[DC_MAXJ + 1];
     __shared__ double rinv_s, q_s;
     if (VTK_XUP_FUSED && __builtin_nontemporal_load(&st->xup_tag) == j) {
-        dc_xupdate(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m);
+        dc_xupdate(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m, nullptr);
         return;
     }
     if (stopped(&st->stop_col, j)) return;
