@@ -20,6 +20,7 @@
     } while (0)
 
 constexpr int NV = 20;
+__constant__ int64_t LDV;   // vector stride in doubles (n + pad)
 
 template <bool NT>
 __device__ __forceinline__ double ld(const double *p) {
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256) void k_rows8(const double *__restrict__ V, int
         double a = 0.0, b = 0.0;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const double v = ld<NT>(V + (size_t)k * n + i);
+            const double v = ld<NT>(V + (size_t)k * LDV + i);
             a += v;
             b -= v;
         }
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256) void k_rows16(const double *__restrict__ V, in
         double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const double2 v = ld2<NT>(reinterpret_cast<const double2 *>(V + (size_t)k * n) + i);
+            const double2 v = ld2<NT>(reinterpret_cast<const double2 *>(V + (size_t)k * LDV) + i);
             ax += v.x;
             ay += v.y;
             bx -= v.x;
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(T) void k_walk(const double *__restrict__ V, int64_
                 double a = 0.0, c = 0.0;
 #pragma unroll
                 for (int k = 0; k < NV; ++k) {
-                    const double v = ld<NT>(V + (size_t)k * n + i);
+                    const double v = ld<NT>(V + (size_t)k * LDV + i);
                     a += v;
                     c -= v;
                 }
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(T) void k_walk(const double *__restrict__ V, int64_
                 double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;
 #pragma unroll
                 for (int k = 0; k < NV; ++k) {
-                    const double2 v = ld2<NT>(reinterpret_cast<const double2 *>(V + (size_t)k * n) + i);
+                    const double2 v = ld2<NT>(reinterpret_cast<const double2 *>(V + (size_t)k * LDV) + i);
                     ax += v.x;
                     ay += v.y;
                     bx -= v.x;
@@ -140,10 +141,14 @@ int main(int argc, char **argv) {
     CHK(hipGetDevice(&dev));
     CHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     double *V, *o0, *o1;
-    CHK(hipMalloc(&V, sizeof(double) * NV * n));
+    const int64_t pad = argc > 2 ? std::atoll(argv[2]) : 0;
+    const int64_t ldv = n + pad;
+    CHK(hipMemcpyToSymbol(HIP_SYMBOL(LDV), &ldv, sizeof ldv));
+    std::printf("n %lld pad %lld doubles\n", (long long)n, (long long)pad);
+    CHK(hipMalloc(&V, sizeof(double) * NV * ldv));
     CHK(hipMalloc(&o0, sizeof(double) * n));
     CHK(hipMalloc(&o1, sizeof(double) * n));
-    CHK(hipMemset(V, 0, sizeof(double) * NV * n));
+    CHK(hipMemset(V, 0, sizeof(double) * NV * ldv));
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
