@@ -70,7 +70,7 @@ for s in "$@"; do
                step slab_c3_1 300 python bench.py --config C3 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
                step slab_c4_8 300 python bench.py --config C4 --slab 8 --comm-solo --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
         benchc2full) step benchc2full 600 python bench.py --config C2 ;;
-        abband) for rep in 1 2; do for v in ${BAND_VARIANTS:-cur wg}; do L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; impl=wave; case $v in cur) ;; wg) impl=wg ;; *) L=tools/bin/lib_$v/libvtkrylov.so ;; esac; VTK_LIB=$L VTK_PROF_PERJ=1 VTK_BAND_IMPL=$impl step abband_${v}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 ${BENCH_ARGS:-} || exit $?; python tools/band_perj.py gpurun_out/abband_${v}_$rep.log; done; done ;;
+        abband) for rep in 1 2; do for v in ${BAND_VARIANTS:-cur wg}; do L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; ch=1; case $v in cur) ;; nochain) ch=0 ;; *) L=tools/bin/lib_$v/libvtkrylov.so ;; esac; VTK_BAND_CHAIN=$ch VTK_LIB=$L VTK_PROF_PERJ=1 step abband_${v}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 ${BENCH_ARGS:-} || exit $?; python tools/band_perj.py gpurun_out/abband_${v}_$rep.log; done; done ;;
         mr4dbg) VTK_DEBUG_BAND=1 step mr4dbg 300 python -u -m pytest tests/test_gpu_multirank.py -x -v -s -k "S2-4" -p no:cacheprovider --timeout 200 --timeout-method thread ;;
         mrlarge) step mrlarge 900 python -u -m pytest tests/test_gpu_multirank_large.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
         sqband) for impl in wg wave; do VTK_BAND_IMPL=$impl step sqband_$impl 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT -d gpurun_out/sqband_$impl -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 2 || exit $?; done ;;

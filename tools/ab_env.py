@@ -1,0 +1,68 @@
+"""In-process A/B of a library environment switch (one operator, one allocation, alternating
+settings): the band step's rate varies ~5 % between processes with the physical placement of
+the same allocations (profiles/r03_membench_walk.txt), so A/Bs across processes need many reps.
+
+    python tools/ab_env.py --env VTK_BAND --values 1,0 --rounds 6 [--config C3] [--slab 8 --comm-solo]
+
+Prints one JSON line: per value the solve wall times (ms) and their median.  The switch must be
+one the library reads per solve (VTK_BAND; VTK_BAND_CHAIN of the dropped band-tail experiment,
+profiles/r03_chain_ab.json)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vt-precondition_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--env", required=True)
+    ap.add_argument("--values", default="1,0")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--slab", type=int, default=1, help="one rank's x-slab at this many GPUs (as bench.py --slab)")
+    ap.add_argument("--comm-solo", action="store_true", help="the distributed code path on one rank (bench.py --comm-solo)")
+    a = ap.parse_args()
+    import vtkrylov as vk
+    from oracle import twin
+    p = twin.CONFIGS[a.config]
+    ctx = vk.default_context(0)
+    if a.comm_solo:
+        os.environ["VTK_COMM_SOLO"] = "1"
+        ctx.comm_init(0, 1, vk.Context.unique_id())
+    shape = (p.shape[0] // a.slab,) + tuple(p.shape[1:])
+    n = int(np.prod(shape))
+    A = vk.vlasov_operator(vk.vlasov_params(p.dim, shape, fp32=p.fp32), ctx=ctx)
+    M = vk.block_jacobi(A, 8)
+    import torch
+    b = torch.from_numpy(vk.rhs_splitmix(n)).to(torch.device("cuda", 0))   # device-resident, as bench.py
+    torch.cuda.synchronize()
+    vals = a.values.split(",")
+    times = {v: [] for v in vals}
+    iters = {}
+    for r in range(a.rounds + 1):
+        for v in (vals if r % 2 == 0 else vals[::-1]):
+            os.environ[a.env] = v
+            t = time.perf_counter()
+            _, info = vk.gmres(A, b, rtol=a.rtol, M=M)
+            dt = (time.perf_counter() - t) * 1e3
+            st = vk.last_stats()
+            iters[v] = (st.inner_iters, st.band, info)
+            if r > 0:   # round 0: warm-up
+                times[v].append(round(dt, 3))
+    out = {"config": a.config, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,
+           "median_ms": {v: statistics.median(t) for v, t in times.items()}, "ms": times}
+    print(json.dumps(out))
+    M.close()
+    A.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1022,7 +1022,9 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const size_t ndc = dc ? (size_t)(m + 1) * (m + 1) + sizeof(DcCoef) / 8 + 8 + (size_t)DC_NQ * GMAX : 0;
     // line-band DCGS2 step: one rank, SELL of uniform width 5 with coded columns (no wide chunk),
     // f64 values, tridiagonal BJ(8) (the fused step's TRIM apply), restart <= 20
-    static const bool band_env = [] { const char *e = std::getenv("VTK_BAND"); return !(e && e[0] == '0'); }();
+    // VTK_BAND=0: the band step off (read per solve: tools/ab_env.py alternates it in one process)
+    const char *band_e = std::getenv("VTK_BAND");
+    const bool band_env = !(band_e && band_e[0] == '0');
     s.band = dc && band_env && c->band && A->band_L > 0 && A->band_L % 8 == 0 &&
              (!c->dist || !A->band_ghost || c->comm || c->host_comm) &&
              A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
