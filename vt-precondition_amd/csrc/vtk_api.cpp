@@ -840,7 +840,10 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
     // (folding the finalize into the boundary launch's last workgroup was measured slower: one
     // workgroup summing 2j+3 x ~1000 partials took as long as the 2j+3-workgroup launch)
-    auto reduce_step = [&](int j, const double *w, int tag, int cnt) -> int {
+    // ev_ar (distributed): recorded on the main stream right after the all-reduce, so a
+    // communication the caller then issues on the comm stream starts only once the all-reduce
+    // has finished: every RCCL operation of the communicator runs in one order, on every rank
+    auto reduce_step = [&](int j, const double *w, int tag, int cnt, hipEvent_t ev_ar = nullptr) -> int {
         if (cnt == 0) {
             Prof pf(c, "dc_dots", tag, n8 * (j + (w ? 2 : 1)));
             HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, tag, c->stream));
@@ -850,8 +853,11 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         if (c->dist) {
             { Prof pf(c, "dc_finalize", tag, 0.0);
               HIPCHK(c, launch_dc_finalize(s.dcpart, cnt, j, w != nullptr, c->d_scal, stop, tag, c->stream)); }
-            Prof pf(c, "allreduce", tag, 8.0 * DC_NQ);
-            TRY(comm_allreduce(c, c->d_scal, DC_NQ));
+            {
+                Prof pf(c, "allreduce", tag, 8.0 * DC_NQ);
+                TRY(comm_allreduce(c, c->d_scal, DC_NQ));
+            }
+            if (ev_ar) HIPCHK(c, hipEventRecord(ev_ar, c->stream));
             part = nullptr;
         }
         Prof pf(c, "dc_scalar", tag, 0.0);
@@ -923,11 +929,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
         }
         // distributed band step: the x-neighbours' edge lines of v_{j-1} and w_j travel to the
-        // ghost buffers on the comm stream (after this step's all-reduce in RCCL order, overlapping
-        // the scalar step); the band step waits for them
+        // ghost buffers on the comm stream once this step's all-reduce has finished (ev_pack:
+        // the RCCL operations never overlap; the exchange overlaps the scalar step); the band
+        // step waits for them
         const bool ghost_x = band && s.ghost && j <= m - 2;
-        if (ghost_x) HIPCHK(c, hipEventRecord(c->ev_pack, c->stream));
-        TRY(reduce_step(j, w_cur, j, cnt));
+        TRY(reduce_step(j, w_cur, j, cnt, ghost_x && c->dist ? c->ev_pack : nullptr));
+        if (ghost_x && !c->dist) HIPCHK(c, hipEventRecord(c->ev_pack, c->stream));
         if (ghost_x) {
             vtk_csr *A = s.A;
             const int L = (int)A->band_L;
