@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--prec", default="bj", choices=["bj", "line"])
+    ap.add_argument("--seg", type=int, default=25)
     ap.add_argument("--slab", type=int, default=1, help="one rank's x-slab at this many GPUs (as bench.py --slab)")
     ap.add_argument("--comm-solo", action="store_true", help="the distributed code path on one rank (bench.py --comm-solo)")
     a = ap.parse_args()
@@ -40,7 +42,8 @@ def main():
     shape = (p.shape[0] // a.slab,) + tuple(p.shape[1:])
     n = int(np.prod(shape))
     A = vk.vlasov_operator(vk.vlasov_params(p.dim, shape, fp32=p.fp32), ctx=ctx)
-    M = vk.block_jacobi(A, 8)
+    params = vk.vlasov_params(p.dim, shape, fp32=p.fp32)
+    M = vk.line_jacobi(A, vk.vlasov_line_stride(params), a.seg) if a.prec == "line" else vk.block_jacobi(A, 8)
     import torch
     b = torch.from_numpy(vk.rhs_splitmix(n)).to(torch.device("cuda", 0))   # device-resident, as bench.py
     torch.cuda.synchronize()
@@ -57,7 +60,7 @@ def main():
             iters[v] = (st.inner_iters, st.band, info)
             if r > 0:   # round 0: warm-up
                 times[v].append(round(dt, 3))
-    out = {"config": a.config, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,
+    out = {"config": a.config, "prec": a.prec, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,
            "median_ms": {v: statistics.median(t) for v, t in times.items()}, "ms": times}
     print(json.dumps(out))
     M.close()
