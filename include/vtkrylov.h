@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTK_ABI_VERSION 3
+#define VTK_ABI_VERSION 4
 
 typedef struct vtk_ctx vtk_ctx;
 typedef struct vtk_csr vtk_csr;
@@ -215,6 +215,13 @@ int vtk_csr_layout_info(vtk_csr *A, vtk_layout_info *out);
  * Same operator, same update arithmetic. */
 int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len);
 int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len);
+/* *separable = 1 when the line band is set and the operator's values are line-separable: every
+ * coupling to line x+-1 depends only on the position v in the line, every coupling to v+-1 in
+ * the same line only on the line x (the 2D Vlasov operators: advection in x with speed v, force
+ * along v with field E(x)).  Checked bit for bit against the CSR when the band is set; the band
+ * step then reads the diagonal per row and those couplings from per-position / per-line tables
+ * (8 B of values per row instead of 40; the same values, summed in the same order).  ABI 4. */
+int vtk_csr_get_line_values(vtk_csr *A, int *separable);
 
 /* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged
  * internally over RCCL when world > 1).  Bit-identical to csr_matvec (serial row sums). */

@@ -163,3 +163,51 @@ def test_band_other_line_lengths(vk_lib, gpu, shape):
     assert np.linalg.norm(xb - ref.x) / np.linalg.norm(ref.x) < 1e-9
     M.close()
     A.close()
+
+
+@pytest.mark.parametrize("name", ["S2", "C1"])
+def test_band_line_separable_values_bit_identical(vk_lib, gpu, name):
+    """The 2D Vlasov operators' values are line-separable (x couplings per position v, v couplings
+    per line x; vtk_csr_get_line_values): the band step reads them from the tables -- the same
+    values summed in the same order as from the SELL copy, so x is bit-identical with
+    VTK_BAND_LSV=0 (read per solve)."""
+    import os
+    p, A = _op(vk_lib, gpu, name)
+    assert A.line_separable
+    M = vk_lib.block_jacobi(A, 8)
+    b = twin.rhs(p.n)
+    x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+    os.environ["VTK_BAND_LSV"] = "0"
+    try:
+        x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+    finally:
+        del os.environ["VTK_BAND_LSV"]
+    assert s1.band == s0.band == 1 and i1 == i0 == 0 and s1.inner_iters == s0.inner_iters
+    assert np.array_equal(x1, x0), "line-separable values change the band step's bits"
+    M.close()
+    A.close()
+
+
+def test_band_not_separable_falls_back(vk_lib, gpu):
+    """One x coupling perturbed: still a line-band operator, no longer line-separable -- the band
+    step reads the SELL values and the solve still meets the oracle on the perturbed matrix."""
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = coracle.generate(p)
+    import scipy.sparse as sp
+    d = d.copy()
+    L = p.shape[1]
+    r = 5 * L + 7   # an interior row; its x+1 coupling (column r + L)
+    k = ip[r] + int(np.nonzero(ix[ip[r]:ip[r + 1]] == r + L)[0][0])
+    d[k] *= 1.0 + 1e-6
+    A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    A.set_line_band(L)
+    assert A.line_band == L and not A.line_separable
+    M = vk_lib.block_jacobi(A, 8)
+    b = coracle.rhs(p.n)
+    x, info, st = _solve(vk_lib, gpu, A, M, b, True)
+    assert st.band == 1 and info == 0
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    assert abs(st.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    M.close()
+    A.close()

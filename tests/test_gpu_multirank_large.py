@@ -51,6 +51,7 @@ def _worker(rank, world, port, case, outdir):
     np.save(os.path.join(outdir, f"x{rank}.npy"), x)
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), info=info, iters=st.inner_iters, band=st.band,
              rb=rb, re=re_, halo=A.n_halo, line_band=A.line_band, mode=M.mode, layout=A.layout_info()["layout"],
+             separable=A.line_separable,
              errors=np.array(hc.errors, dtype=object).astype(str))
     M.close()
     A.close()
@@ -77,6 +78,7 @@ def test_row_partitioned_full_size(tmp_path, golden_large, case, world):
         if p.dim == 2:   # the line-band step across ranks: halo = the two neighbour lines
             assert int(z["line_band"]) == p.shape[1] and int(z["halo"]) == 2 * p.shape[1]
             assert int(z["band"]) == 1
+            assert bool(z["separable"])   # the distributed line-separable tables (halo lines)
         else:            # 4D: the halo is the two neighbour x-planes
             assert int(z["halo"]) == 2 * int(np.prod(p.shape[1:]))
         iters.append(int(z["iters"]))

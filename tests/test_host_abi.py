@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(vk_lib):
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(vk_lib._abi.PROTOTYPES), set(names) ^ set(vk_lib._abi.PROTOTYPES)
-    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 3
+    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 4
 
 
 def test_status_strings(vk_lib):

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_rows16(const double *__restrict__ V, in
 
 // the band step's walk: workgroup (range r, part h) reads rows [x L + h LP, + LP) of its lines
 // x in order, one row per lane (T threads, LP rows: lanes >= LP idle) or two (RPL = 2)
-template <bool NT, int RPL, int T, int MODE = 0>
+template <bool NT, int RPL, int T, int MODE = 0, int NBAR = 0>
 __global__ __launch_bounds__(T) void k_walk(const double *__restrict__ V, int64_t n, int L, int H,
                                             double *__restrict__ o0, double *__restrict__ o1) {
     const int LP = L / H, X = (int)(n / L);
@@ -112,6 +112,8 @@ __global__ __launch_bounds__(T) void k_walk(const double *__restrict__ V, int64_
                 __builtin_nontemporal_store(a, o0 + i);
                 __builtin_nontemporal_store(c, o1 + i);
             }
+#pragma unroll
+            for (int q = 0; q < NBAR; ++q) __syncthreads();   // the band step's barriers per line
         } else {
             if (2 * t < LP) {
                 const int64_t i = (row0 >> 1) + t;
@@ -194,6 +196,8 @@ int main(int argc, char **argv) {
         run("walk 8B nt T448 rotated", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 1>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });
         run("walk 8B nt T448 interleaved", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 2>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });
         run("walk 16B nt T256 rotated", [&] { hipLaunchKernelGGL((k_walk<true, 2, 256, 1>), dim3(R * H), dim3(256), 0, 0, V, n, L, H, o0, o1); });
+        run("walk 8B nt T448 1 barrier", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 0, 1>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });
+        run("walk 8B nt T448 3 barriers", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 0, 3>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });
         run("walk 8B nt T448 chunk 8", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 8>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });
         run("walk 8B nt T448 chunk 16", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 16>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });
         run("walk 8B nt T448 chunk 32", [&] { hipLaunchKernelGGL((k_walk<true, 1, 448, 32>), dim3(R * H), dim3(448), 0, 0, V, n, L, H, o0, o1); });

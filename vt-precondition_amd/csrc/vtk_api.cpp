@@ -614,6 +614,7 @@ void destroy_csr(vtk_csr *A) {
     (void)hipFree(A->d_halo);
     (void)hipFree(A->d_send_idx);
     (void)hipFree(A->d_send_buf);
+    (void)hipFree(A->d_lsv);
     free_sell(A);
     (void)hipFree(A->g_in.d_list);
     (void)hipFree(A->g_bd.d_list);
@@ -745,6 +746,28 @@ int band_check_all(vtk_csr *A, int64_t L) {
     A->band_off_last = chk.lay.off_last;
     A->band_off_left = chk.lay.off_left;
     A->band_off_right = chk.lay.off_right;
+    // line-separable values (rank-local: the band step reads them or the SELL values, the same
+    // bits either way): built and checked against the CSR bit for bit, dropped when they do not
+    // reproduce it (f64 values only)
+    (void)hipFree(A->d_lsv);
+    A->d_lsv = nullptr;
+    const int64_t n = A->n_local;
+    if (!A->fp32 && n % L == 0) {
+        const size_t nl = (size_t)n + 2 * (size_t)L + 2 * (size_t)(n / L);
+        double *lsv = nullptr;
+        HIPCHK(c, hipMalloc(&lsv, nl * sizeof(double)));
+        DBuf bad;
+        TRY(dalloc(c, bad, sizeof(int)));
+        HIPCHK(c, hipMemsetAsync(lsv, 0, nl * sizeof(double), c->stream));
+        HIPCHK(c, hipMemsetAsync(bad.p, 0, sizeof(int), c->stream));
+        HIPCHK(c, launch_lsv_build(A->d_indptr, A->d_indices, static_cast<const double *>(A->d_data), n, (int)L,
+                                   chk.ghost ? chk.lay.lblk : -1, lsv, bad.as<int>(), c->stream));
+        int hb = 1;
+        HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (hb == 0) A->d_lsv = lsv;
+        else (void)hipFree(lsv);
+    }
     return VTK_OK;
 }
 
@@ -866,6 +889,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         return VTK_OK;
     };
     const bool band = s.band;
+    // line-separable values in the band step (VTK_BAND_LSV=0: the SELL values; read per solve)
+    const char *lsv_e = std::getenv("VTK_BAND_LSV");
+    const bool band_lsv = band && s.A->d_lsv && !(lsv_e && lsv_e[0] == '0');
+    // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
+    // the SELL values)
+    const double b_band = band_lsv ? b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n : b_csr;
     bool broke = false;
     static const int ev_every = [] {
         const char *e = std::getenv("VTK_EV_EVERY");
@@ -957,7 +986,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 "band_step_j04", "band_step_j05", "band_step_j06", "band_step_j07", "band_step_j08", "band_step_j09",
                 "band_step_j10", "band_step_j11", "band_step_j12", "band_step_j13", "band_step_j14", "band_step_j15",
                 "band_step_j16", "band_step_j17", "band_step_j18", "band_step_j19"};
-            Prof pf(c, perj && j < 20 ? jname[j] : "band_step", j, b_csr + b_inv + n8 * (j + (j >= 1 ? 4 : 3) + (j == m - 2 ? 1 : 0)));
+            Prof pf(c, perj && j < 20 ? jname[j] : "band_step", j, b_band + b_inv + n8 * (j + (j >= 1 ? 4 : 3) + (j == m - 2 ? 1 : 0)));
             BandK a;
             a.pk = s.A->sell.d_pk;
             a.dict = s.A->sell.d_dict;
@@ -982,6 +1011,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.H_parts = s.band_H;
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
+            a.lsv = band_lsv ? s.A->d_lsv : nullptr;
             HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
@@ -1882,6 +1912,12 @@ int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len) {
 int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len) {
     if (!A || !line_len) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_csr_get_line_band: NULL argument");
     *line_len = A->band_L;
+    return VTK_OK;
+}
+
+int vtk_csr_get_line_values(vtk_csr *A, int *separable) {
+    if (!A || !separable) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_csr_get_line_values: NULL argument");
+    *separable = A->band_L > 0 && A->d_lsv != nullptr ? 1 : 0;
     return VTK_OK;
 }
 

@@ -56,7 +56,10 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 #define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
 #endif
 
-template <int WU, int J, int GEO>
+// LSV: the matrix values from the line-separable tables (vtk_csr::d_lsv: the diagonal per row,
+// x +- 1 couplings per position v -- held in registers for the lane's v --, v +- 1 couplings per
+// line) instead of the SELL copy's 5 values per row: the same values in the same order
+template <int WU, int J, int GEO, bool LSV = false>
 __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
     constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
@@ -80,6 +83,14 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     const bool own = tid >= 8 && tid < 8 + LP;
     const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
     const int ii = lane & 7;
+    // LSV: the lane's x-coupling values (position v in every line)
+    double tx0 = 0.0, tx1 = 0.0;
+    if constexpr (LSV) {
+        if (v >= 0 && v < L) {
+            tx0 = a.lsv[a.n + v];
+            tx1 = a.lsv[a.n + L + v];
+        }
+    }
     for (int k = tid; k < j; k += BAND_T) {
         cs[k] = a.cf->s[k];
         ce[k] = a.cf->e[k];
@@ -195,14 +206,20 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         const int l64 = (int)(row & 63);
         uint32_t word = 0u;
         int dv = 0;
-        double d[WU];
-        double mrow = 1.0;
+        double d[LSV ? 1 : WU];
+        double mrow = 1.0, drow = 0.0, tv0 = 0.0, tv1 = 0.0;
         if (work) {
             word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
             const int64_t qd = q0 + (lane >> 4);
             dv = (lane < 32 && qd >= 0 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
+            if constexpr (LSV) {
+                if (own) drow = __builtin_nontemporal_load(a.lsv + row);
+                tv0 = a.lsv[a.n + 2 * L + x];
+                tv1 = a.lsv[a.n + 2 * L + X + x];
+            } else {
 #pragma unroll
-            for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
+                for (int k = 0; k < WU; ++k) d[k] = __builtin_nontemporal_load(a.val + q * 64 * WU + 64 * k + l64);
+            }
             if (own) mrow = __builtin_nontemporal_load(a.mtri + row);
         }
         // 1. update of line y
@@ -241,9 +258,12 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                     else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
                     else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
                     const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
-                    sacc += d[k] * xv;
-                    if (off == -1 && ii > 0) sub = sub + d[k];
-                    if (off == 1 && ii < 7) sup = sup + d[k];
+                    double dk;
+                    if constexpr (LSV) dk = rel != 0 ? (rel > 0 ? tx1 : tx0) : (vc == v ? drow : (vc > v ? tv1 : tv0));
+                    else dk = d[k];
+                    sacc += dk * xv;
+                    if (off == -1 && ii > 0) sub = sub + dk;
+                    if (off == 1 && ii < 7) sup = sup + dk;
                 }
             }
             const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
@@ -318,7 +338,8 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     switch (a.j) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
-        hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, true>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        else hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         break;
         VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
         VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
@@ -409,6 +430,65 @@ hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices,
     if (g < 1) g = 1;
     hipLaunchKernelGGL(k_band_check_dist, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, n, L, lblk, bad);
     return hipGetLastError();
+}
+
+// line-separable values: the table slot of entry (r, c) -- 0 the diagonal D[r], 1 TX[dir][v]
+// (line x +- 1 at the row's position v), 2 TV[dir][x] (v +- 1 in the row's line) -- or -1
+__device__ __forceinline__ int lsv_slot(int64_t r, int64_t c, int64_t n, int L, int X, int lblk, int64_t &idx) {
+    const int64_t x = r / L, v = r % L;
+    int64_t dx, vc;
+    if (c < n) {
+        dx = c / L - x;
+        vc = c % L;
+        if (lblk < 0) {   // one rank: periodic in x (X >= 3)
+            if (dx == X - 1) dx = -1;
+            else if (dx == -(X - 1)) dx = 1;
+        }
+    } else {
+        const int64_t kk = c - n, blk = kk / L;
+        dx = blk == lblk ? -1 : 1;
+        vc = kk % L;
+    }
+    if (dx == 0) {
+        if (vc == v) { idx = r; return 0; }
+        if (vc == v - 1 || vc == v + 1) { idx = (int64_t)n + 2 * L + (vc > v ? X : 0) + x; return 2; }
+        return -1;
+    }
+    if ((dx == 1 || dx == -1) && vc == v) { idx = (int64_t)n + (dx > 0 ? L : 0) + v; return 1; }
+    return -1;
+}
+
+// pass 0: write every entry into its slot (entries sharing a table slot write the same bits when
+// the operator is separable; the check pass decides); pass 1: compare every entry bit for bit
+__global__ __launch_bounds__(NT) void k_lsv_build(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
+                                                  const double *__restrict__ data, int64_t n, int L, int lblk,
+                                                  double *__restrict__ lsv, int *bad, int pass) {
+    const int X = (int)(n / L);
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
+        for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
+            int64_t idx;
+            if (lsv_slot(r, indices[k], n, L, X, lblk, idx) < 0) {
+                atomicOr(bad, 1);
+                break;
+            }
+            if (pass == 0) lsv[idx] = data[k];
+            else if (__double_as_longlong(lsv[idx]) != __double_as_longlong(data[k])) atomicOr(bad, 1);
+        }
+    }
+}
+
+hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const double *data, int64_t n, int L,
+                            int lblk, double *lsv, int *bad, hipStream_t s) {
+    if (L <= 0 || n % L != 0 || n / L < 2) return hipErrorInvalidValue;
+    int64_t g = (n + NT - 1) / NT;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    for (int pass = 0; pass < 2; ++pass) {
+        hipLaunchKernelGGL(k_lsv_build, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, data, n, L, lblk, lsv, bad, pass);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // *bad |= 1 when a column lies outside lines x-1..x+1 (mod X) of its row's line x; |= 2 when it

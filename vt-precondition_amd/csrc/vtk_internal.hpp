@@ -176,8 +176,14 @@ struct vtk_csr {
     int64_t n_send = 0;
     int64_t band_L = 0;                                 // line-band structure (vtk_csr_set_line_band)
     bool band_vloc = false;                             // ... with every column within v-1..v+1 of its row
+    // line-separable values (k_lsv_build): every coupling to line x+-1 depends
+    // only on the position v (table TX[2][L]), every coupling to v+-1 in the same line only on
+    // the line x (TV[2][X]), the diagonal per row (D[n]) -- verified bit-exactly against the CSR
+    // when the band is set; the band step then reads 8 B of values per row instead of 40.
+    // d_lsv = D | TX | TV; null: not separable (the band step reads the SELL values)
+    double *d_lsv = nullptr;
     // distributed band step: the halo is two neighbour lines; peers and the alltoallv layout of
-    // the per-step ghost exchange (3 L doubles per side), -1 offsets: no such side
+    // the per-step ghost exchange (BAND_GHOST_VECS L doubles per side), -1 offsets: no such side
     bool band_ghost = false;                            // band across ranks: per-step ghost exchange
     int band_lblk = 0;
     int band_peer[2] = {-1, -1};                        // left, right neighbour rank
@@ -375,6 +381,7 @@ struct BandK {
                                  // v_k (k < j) and w_j, w_{j-1} by parity in slots m, m+1
                                  // (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
+    const double *lsv;           // line-separable values (vtk_csr::d_lsv) or null: SELL values
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
 // geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
@@ -391,6 +398,11 @@ hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off
 int band_parts(int64_t L);    // parts per line (rows per part <= BAND_LP, multiple of 8); 0: none (vtk_host.cpp)
 // *bad |= 1 when some column is outside the lines x-1..x+1 (mod X) of its row, |= 2 when one is
 // more than one row off its row's position in the line (bad zeroed by the caller)
+// line-separable values (vtk_csr::d_lsv): build D | TX | TV from the CSR, then *bad |= 1 when
+// some entry is not reproduced bit-exactly (or is no diagonal / v+-1 / same-position x+-1
+// coupling).  lblk < 0: one rank (x couplings periodic); else the halo block of the left line
+hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const double *data, int64_t n, int L,
+                            int lblk, double *lsv, int *bad, hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 

@@ -228,6 +228,15 @@ class CsrOperator:
         check(lib().vtk_csr_get_line_band(self._h, C.byref(v)), self.ctx.handle)
         return v.value
 
+    @property
+    def line_separable(self) -> bool:
+        """True when the band step reads the values from per-position / per-line tables (the
+        operator's x couplings depend only on v, its v couplings only on x; checked bit for bit
+        when the band was set -- vtk_csr_get_line_values)."""
+        v = C.c_int()
+        check(lib().vtk_csr_get_line_values(self._h, C.byref(v)), self.ctx.handle)
+        return bool(v.value)
+
     def layout_info(self) -> dict:
         """Layout in use, bytes of the operator one SpMV reads in it, SELL chunk counts."""
         li = _abi.LayoutInfo()

@@ -88,6 +88,7 @@ PROTOTYPES = {
     "vtk_csr_layout_info": (C.c_int, [P, C.c_void_p]),
     "vtk_csr_set_line_band": (C.c_int, [P, C.c_int64]),
     "vtk_csr_get_line_band": (C.c_int, [P, I64P]),
+    "vtk_csr_get_line_values": (C.c_int, [P, C.POINTER(C.c_int)]),
     "vtk_bjacobi_get_mode": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_destroy": (None, [P]),
     "vtk_linejacobi_create": (C.c_int, [P, C.c_int64, C.c_int64, C.POINTER(P)]),
@@ -106,7 +107,7 @@ PROTOTYPES = {
 }
 
 
-ABI_VERSION = 3   # include/vtkrylov.h VTK_ABI_VERSION
+ABI_VERSION = 4   # include/vtkrylov.h VTK_ABI_VERSION
 
 
 class BandGeometry(C.Structure):
