@@ -417,7 +417,10 @@ def main():
     #     columns, no residual SpMV for x0 = 0 -- fewer bytes, not skipped work)
     n_loc, nnz_loc = A.n_local, A.nnz
     csr_matrix_bytes = (4 if fp32 else 8) * nnz_loc + 4 * nnz_loc + 4 * (n_loc + 1)
-    d_matrix = csr_matrix_bytes - linfo["matrix_bytes"]
+    # the band step reads the SELL codes and -- line-separable operators (A.line_separable) --
+    # 8 B of values per row from the diagonal table instead of the SELL values (vtk_api.cpp b_band)
+    band_matrix = linfo["matrix_bytes"] - (8.0 * linfo["sell_entries"] - 8.0 * n_loc if A.line_separable else 0.0)
+    d_matrix = csr_matrix_bytes - (band_matrix if dom == "band_step" else linfo["matrix_bytes"])
     dom_csr = dk["bytes"] / dk["launches"] + (d_matrix if dom.startswith("spmv") or dom == "band_step" else 0.0)
     solve_bytes = sum(v["bytes"] for v in kprof.values())
     it_solve = int(round(iters / args.steps))
@@ -428,28 +431,16 @@ def main():
     sec8d = sum(B_spmv + B_pc + 8 * n_loc * (2 * (k % m) + 8) for k in range(it_solve)) \
         + cycles * (B_spmv + 24 * n_loc + B_pc + 24 * n_loc + 8 * n_loc * (m + 2))
     t_solve = ms / 1e3
-    # the band step does the work of the fused SpMV+BJ+dots kernel AND the update
-    # pass; those two would read the basis once more per launch (8 n j bytes).  Its algorithmic
-    # bytes per launch are matrix + m + 8 n (j + 6), so sum_j 8 n j = bytes - launches * (matrix
-    # + m + 48 n): the unfused-equivalent bytes and rate of the same work.
+    # (round 2's "unfused-equivalent" band rate is no longer reported: with p_j recomputed and
+    # the line-separable values the band step's bytes per launch differ from the two kernels' by
+    # more than one basis read, and the per-j mix of a solve is not in the aggregate profile)
     band_equiv = None
-    if "band_step" in kprof:
-        bk = kprof["band_step"]
-        fixed = linfo["matrix_bytes"] + 8.0 * n_loc + 48.0 * n_loc
-        extra = bk["bytes"] - bk["launches"] * fixed
-        eq = (bk["bytes"] + extra) / bk["launches"]
-        band_equiv = {"kernel": "band_step", "bytes_per_launch": bk["bytes"] / bk["launches"],
-                      "unfused_equiv_bytes_per_launch": eq, "avg_us": bk["avg_us"],
-                      "unfused_equiv_gbs": eq / (bk["avg_us"] * 1e-6) / 1e9,
-                      "unfused_equiv_frac": eq / (bk["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                      "note": "bytes the fused SpMV+BJ+dots kernel and the update pass would move for the "
-                              "same step (one more basis read) / the band step's time"}
     recon = {
         "note": "SURVEY 8(d) reconciliation; per rank (n_local rows); frac = GB/s / 8000",
         "dominant_kernel_csr_equiv": {"kernel": dom, "bytes_per_launch": dom_csr,
                                       "gbs": dom_csr / (dk["avg_us"] * 1e-6) / 1e9,
                                       "frac": dom_csr / (dk["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                                      "matrix_bytes_layout": linfo["matrix_bytes"],
+                                      "matrix_bytes_layout": band_matrix if dom == "band_step" else linfo["matrix_bytes"],
                                       "matrix_bytes_csr_int32": csr_matrix_bytes},
         "solve_actual": {"bytes": solve_bytes, "gbs": solve_bytes / t_solve / 1e9,
                          "frac": solve_bytes / t_solve / 1e9 / HBM_PEAK_GBS,
