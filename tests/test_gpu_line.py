@@ -295,3 +295,28 @@ def test_gmres_line_full_size(gpu, vk_lib, name):
     M.close()
     vk.gmres(A, b, rtol=1e-8, M=vk.block_jacobi(A, 8))
     assert it_line * 1.5 < vk.last_stats().inner_iters
+
+
+def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
+    """On a line-separable operator the line path's SpMV reads the values from the tables
+    (k_lsv_spmv): k_sell's plain sum in the same order, so the solve is
+    bit-identical with VTK_BAND_LSV=0 (the SELL values; read per solve)."""
+    import os
+    import numpy as np
+    from oracle import twin
+    p = twin.CONFIGS["C1"]
+    A = vk_lib.vlasov_operator(vk_lib.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=gpu)
+    assert A.line_separable
+    M = vk_lib.line_jacobi(A, vk_lib.vlasov_line_stride(vk_lib.vlasov_params(p.dim, p.shape)), 25)
+    b = twin.rhs(p.n)
+    x1, i1 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
+    it1 = vk_lib.last_stats().inner_iters
+    os.environ["VTK_BAND_LSV"] = "0"
+    try:
+        x0, i0 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
+    finally:
+        del os.environ["VTK_BAND_LSV"]
+    assert i1 == i0 == 0 and it1 == vk_lib.last_stats().inner_iters
+    assert np.array_equal(x1, x0)
+    M.close()
+    A.close()

@@ -857,8 +857,14 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
     const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
                          s.M->line.seg <= 32 && s.G <= GMAX;
+    // line path on a line-separable operator: the SpMV from the tables (VTK_BAND_LSV=0: SELL)
+    const char *lsv_e0 = std::getenv("VTK_BAND_LSV");
+    const bool line_lsv = line_dc && s.A->d_lsv && s.A->band_L > 0 && !(lsv_e0 && lsv_e0[0] == '0') && s.A->use_sell &&
+                          s.A->sell.uniform_w == 5 && s.A->sell.d_pk && s.A->sell.n_wide == 0 &&
+                          (!c->dist || s.A->band_ghost);
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = matrix_bytes(s.A);
+    const double b_lsv = b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n;
     const double b_inv = bj_row_bytes(s.M) * n;
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
     // (folding the finalize into the boundary launch's last workgroup was measured slower: one
@@ -947,9 +953,17 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         } else if (line_dc) {
             // line path: SpMV, then the line sweeps with the step's dots fused behind them
             TRY(halo_exchange(s.A, pj));
-            { Prof pf(c, "spmv", j, b_csr + 2 * n8);
-              HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
-                                    nullptr, stop, j, c->stream)); }
+            if (line_lsv) {
+                // line-separable values: 12 B of matrix per row (codes + diagonal)
+                Prof pf(c, "spmv_lsv", j, b_lsv + 2 * n8);
+                HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
+                                          s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
+                                          c->stream));
+            } else {
+                Prof pf(c, "spmv", j, b_csr + 2 * n8);
+                HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
+                                      nullptr, stop, j, c->stream));
+            }
             { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
               HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream)); }
             cnt = s.G;

@@ -3,6 +3,7 @@
 // SpMV and block-Jacobi arithmetic is bit-identical to k_dc_update / k_sell.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "vtk_device.hpp"
@@ -489,6 +490,63 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// y = A x from the line-separable tables and the SELL codes (one wave per 64-row chunk, lane per
+// row): k_sell's plain SpMV -- entries in stored order, padding skipped -- reading 12 B of
+// matrix per row instead of 44.  lblk < 0: one rank (x couplings periodic); else the halo
+// block of the left neighbour line (HALO: the halo columns read from halo[])
+template <bool HALO>
+__global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk, const int32_t *__restrict__ dict,
+                                                 const double *__restrict__ lsv, const double *__restrict__ x,
+                                                 const double *__restrict__ halo, double *__restrict__ y, int n, int L,
+                                                 int lblk, const int *stop_col, int col) {
+    if (stopped(stop_col, col)) return;
+    const int lane = threadIdx.x & 63;
+    const int X = n / L, nch = (n + 63) >> 6;
+    for (int q = (int)(((int64_t)blockIdx.x * NT + threadIdx.x) >> 6); q < nch; q += (int)((int64_t)gridDim.x * NT >> 6)) {
+        const int r = 64 * q + lane;
+        const bool act = r < n;
+        const uint32_t word = act ? __builtin_nontemporal_load(pk + (size_t)q * 64 + lane) : ~0u;
+        const int dv = lane < 16 ? dict[(size_t)q * 16 + lane] : 0;
+        // the row's line and position: the chunk's first row by one division, then the lane
+        int xl = (64 * q) / L, v = 64 * q - xl * L + lane;
+        while (v >= L) {
+            v -= L;
+            ++xl;
+        }
+        const double drow = act ? __builtin_nontemporal_load(lsv + r) : 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int code = (int)((word >> (4 * k)) & 15u);
+            const int off = __shfl(dv, code, 64);
+            if (act && code != PK_CODES) {
+                const int c = r + off;
+                double val;
+                if (off == 0) val = drow;
+                else if (off == 1 || off == -1) val = lsv[(size_t)n + 2 * L + (off > 0 ? X : 0) + xl];
+                else {
+                    const bool up = (HALO && c >= n) ? ((c - n) / L != lblk) : (off == L || off == -(X - 1) * L);
+                    val = lsv[(size_t)n + (up ? L : 0) + v];
+                }
+                const double xv = (HALO && c >= n) ? halo[c - n] : x[c];
+                s += val * xv;
+            }
+        }
+        if (act) __builtin_nontemporal_store(s, y + r);
+    }
+}
+
+hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
+                           const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
+                           hipStream_t s) {
+    if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || (halo && lblk < 0)) return hipErrorInvalidValue;
+    const int64_t nch = (n + 63) / 64;
+    const int64_t g = std::max<int64_t>(1, std::min<int64_t>((nch + 3) / 4, 2048));
+    if (halo) hipLaunchKernelGGL(k_lsv_spmv<true>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
+    else hipLaunchKernelGGL(k_lsv_spmv<false>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
+    return hipGetLastError();
 }
 
 // *bad |= 1 when a column lies outside lines x-1..x+1 (mod X) of its row's line x; |= 2 when it

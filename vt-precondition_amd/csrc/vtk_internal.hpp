@@ -403,6 +403,11 @@ int band_parts(int64_t L);    // parts per line (rows per part <= BAND_LP, multi
 // coupling).  lblk < 0: one rank (x couplings periodic); else the halo block of the left line
 hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const double *data, int64_t n, int L,
                             int lblk, double *lsv, int *bad, hipStream_t s);
+// y = A x from the line-separable tables and the SELL codes (uniform width 5, coded columns):
+// k_sell's plain SpMV, the same bits.  halo != null: the distributed layout (lblk the left block)
+hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
+                           const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
+                           hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 
