@@ -211,3 +211,25 @@ def test_band_not_separable_falls_back(vk_lib, gpu):
     assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-9
     M.close()
     A.close()
+
+
+@pytest.mark.parametrize("orth", ["dcgs2", "mgs"])
+def test_separable_values_in_unfused_paths_bit_identical(vk_lib, gpu, orth):
+    """The solver's other SELL launches (fused SpMV + BJ + dots, residual, MGS matvec) also read
+    the line-separable tables on such operators: with the band step off, x is bit-identical with
+    VTK_BAND_LSV=0 for both orthogonalisations."""
+    import os
+    p, A = _op(vk_lib, gpu, "C1")
+    assert A.line_separable
+    M = vk_lib.block_jacobi(A, 8)
+    b = twin.rhs(p.n)
+    x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
+    os.environ["VTK_BAND_LSV"] = "0"
+    try:
+        x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
+    finally:
+        del os.environ["VTK_BAND_LSV"]
+    assert s1.band == s0.band == 0 and i1 == i0 == 0 and s1.inner_iters == s0.inner_iters
+    assert np.array_equal(x1, x0)
+    M.close()
+    A.close()

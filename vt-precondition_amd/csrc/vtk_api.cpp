@@ -324,10 +324,33 @@ bool bj_fused(const vtk_prec *M) {
     return M->fused;
 }
 
+// the solver's SELL launches read the line-separable tables when the operator
+// has them: the same values, the same sums, 8 B of values per row instead of 40 (VTK_BAND_LSV=0:
+// the SELL values; read per call).  vtk_spmv keeps the SELL values: it is the measured SpMV
+bool lsv_on(const vtk_csr *A) {
+    const char *e = std::getenv("VTK_BAND_LSV");
+    return A->use_sell && A->d_lsv && A->band_L > 0 && !A->fp32 && !(e && e[0] == '0') &&
+           (!A->ctx->dist || A->band_ghost);
+}
+SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
+    if (in.sell && lsv_on(A)) {
+        in.lsv = A->d_lsv;
+        in.lsv_L = (int)A->band_L;
+        in.lsv_lblk = A->band_ghost ? A->band_lblk : -1;
+    }
+    return in;
+}
+double matrix_bytes(const vtk_csr *A);
+// matrix bytes a solver SELL launch reads (lsv_in)
+double solver_matrix_bytes(const vtk_csr *A) {
+    const double b = matrix_bytes(A);
+    return lsv_on(A) ? b - 8.0 * (double)A->sell.entries + 8.0 * (double)A->n_local : b;
+}
+
 // interior / boundary pieces of the fused SpMV (world > 1)
 bool bj_split(const vtk_prec *M) { return M && (M->A->use_sell ? M->A->g_in.grid > 0 : M->split); }
 SpmvIn split_in(vtk_csr *A, vtk_prec *M, const double *x, bool interior) {
-    return interior ? spmv_in(A, &M->tiles_in, x, &A->g_in) : spmv_in(A, &M->tiles_bd, x, &A->g_bd);
+    return lsv_in(interior ? spmv_in(A, &M->tiles_in, x, &A->g_in) : spmv_in(A, &M->tiles_bd, x, &A->g_bd), A);
 }
 
 // Build the halo plan of a freshly uploaded CSR (indices still GLOBAL on the device), remap
@@ -807,23 +830,23 @@ int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int c
     TRY(halo_exchange(A, v));
     const double *v0 = want_dots ? s.V : nullptr;
     const double n8 = 8.0 * s.n;
-    const double b_csr = matrix_bytes(A);
+    const double b_csr = solver_matrix_bytes(A);
     const double b_inv = bj_row_bytes(s.M) * s.n;
     int cnt;
     if (!s.M) {
         Prof pf(c, "spmv_w", col, b_csr + 3 * n8);
-        const SpmvIn in = spmv_in(A, &A->tiles, v);
+        const SpmvIn in = lsv_in(spmv_in(A, &A->tiles, v), A);
         HIPCHK(c, launch_spmv(in, EPI_PREC, w, nullptr, BjOp{}, v0, s.part[0], s.part[1], stop, col, c->stream));
         cnt = spmv_grid(in);
     } else if (bj_fused(s.M)) {
         Prof pf(c, "spmv_bj", col, b_csr + b_inv + 3 * n8);   // x, v0, w + CSR + BJ rows
-        const SpmvIn in = spmv_in(A, &s.M->tiles, v);
+        const SpmvIn in = lsv_in(spmv_in(A, &s.M->tiles, v), A);
         HIPCHK(c, launch_spmv(in, EPI_PREC, w, nullptr, bj_op(s.M), v0, s.part[0], s.part[1], stop, col, c->stream));
         cnt = spmv_grid(in);
     } else {
         {
             Prof pf(c, "spmv", col, b_csr + 2 * n8);
-            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, v), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr, nullptr, stop, col, c->stream));
+            HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, &A->tiles, v), A), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr, nullptr, stop, col, c->stream));
         }
         Prof pf(c, prec_cls(s.M), col, b_inv + 3 * n8);
         HIPCHK(c, launch_bj_apply(bj_op(s.M), s.n, s.tmp, w, v0, s.part[0], s.part[1], s.G, stop, col, c->stream));
@@ -912,7 +935,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     for (int j = 0; j < m; ++j) {
         double *pj = s.V + (size_t)j * s.ld;
         int cnt = 0;
-        const double b_step = b_csr + b_inv + n8 * (j + 2);   // CSR, BJ, p, w, V_j
+        const double b_step = solver_matrix_bytes(s.A) + b_inv + n8 * (j + 2);   // matrix, BJ, p, w, V_j
         // band: step j's w and partials come from the band step j-1 (w in buffer j % 3)
         double *const wb[3] = {s.w, s.tmp, s.w3};
         double *w_cur = band ? wb[j % 3] : s.w;
@@ -947,7 +970,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         } else if (fused) {
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
-            const SpmvIn in = spmv_in(s.A, ft, pj);
+            const SpmvIn in = lsv_in(spmv_in(s.A, ft, pj), s.A);
             HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             cnt = spmv_grid(in);
         } else if (line_dc) {
@@ -1151,7 +1174,6 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(GmresState), hipMemcpyHostToDevice, c->stream));
     int rc;
     const double n8 = 8.0 * n;
-    const double b_spmv = matrix_bytes(A) + 2 * n8;
     const double b_pc = bj_row_bytes(M) * n + 2 * n8;
     // ||b|| and ||M b|| (iterative.py:708, :714)
     { Prof pf(c, "dot", -1, n8);
@@ -1181,23 +1203,22 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const Tiles *rtiles = (M && bj_fused(M)) ? &M->tiles : &A->tiles;
     const SpmvIn rin0 = spmv_in(A, rtiles, x), pin0 = spmv_in(A, &A->tiles, x);
     double *prr = c->d_part + 4 * GMAX, *prz = c->d_part + 5 * GMAX;
-    const double b_csr = matrix_bytes(A);
     Red rz{prz, spmv_grid(rin0)};
     auto residual = [&]() -> int {
         TRY(halo_exchange(A, x));
         int rc2;
         Red rr;
         if (fres) {
-            Prof pf(c, "spmv_resid_bj", -1, b_csr + bj_row_bytes(M) * n + 3 * n8);
-            HIPCHK(c, launch_spmv(spmv_in(A, rtiles, x), EPI_RESID_PREC, s.V, b, bj_op(M),
+            Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
+            HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, rtiles, x), A), EPI_RESID_PREC, s.V, b, bj_op(M),
                                   nullptr, prr, prz, nullptr, 0, c->stream));
             rr = reduce(c, prr, spmv_grid(rin0), rc2);
             TRY(rc2);
             rz = reduce(c, prz, spmv_grid(rin0), rc2);
             TRY(rc2);
         } else {
-            Prof pf(c, "spmv_resid", -1, b_spmv + n8);
-            HIPCHK(c, launch_spmv(spmv_in(A, &A->tiles, x), EPI_RESID, s.r, b, BjOp{}, nullptr, prr, nullptr, nullptr, 0, c->stream));
+            Prof pf(c, "spmv_resid", -1, solver_matrix_bytes(A) + 3 * n8);
+            HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, &A->tiles, x), A), EPI_RESID, s.r, b, BjOp{}, nullptr, prr, nullptr, nullptr, 0, c->stream));
             rr = reduce(c, prr, spmv_grid(pin0), rc2);
             TRY(rc2);
         }

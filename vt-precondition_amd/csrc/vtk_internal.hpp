@@ -226,6 +226,9 @@ struct SpmvIn {
     const double *x, *halo;   // halo may be null (world == 1)
     const Sell *sell = nullptr;
     const Groups *groups = nullptr;
+    // line-separable values (SELL, f64; solver launches only -- vtk_spmv keeps the SELL values)
+    const double *lsv = nullptr;
+    int lsv_L = 0, lsv_lblk = -1;
 };
 
 LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);

@@ -15,6 +15,7 @@
 #include <float.h>
 
 #include <climits>
+#include <type_traits>
 #include <cstdlib>
 
 #include "vtk_internal.hpp"
@@ -59,7 +60,22 @@ struct SpmvK {
     const int64_t *pk_off;
     const int32_t *dict;
     int sell_uw;   // Sell::uniform_w (0: read the offsets)
+    // line-separable values (vtk_csr::d_lsv, solver launches only; null: the SELL values): the
+    // entry's value from its column -- the same value, so the same sums
+    const double *lsv;
+    int lsv_L, lsv_lblk;
 };
+
+// value of entry (row, c) from the line-separable tables; drow = D[row], (xl, v) the row's line
+// and position (vtk_band.hip k_lsv_build)
+template <typename VT, bool HALO>
+__device__ __forceinline__ double lsv_value(const SpmvK<VT, HALO> &a, int row, int c, double drow, int xl, int v) {
+    const int off = c - row, L = a.lsv_L, X = a.n_local / L;
+    if (off == 0) return drow;
+    if (off == 1 || off == -1) return a.lsv[(size_t)a.n_local + 2 * L + (off > 0 ? X : 0) + xl];
+    const bool up = (HALO && c >= a.n_local) ? ((c - a.n_local) / L != a.lsv_lblk) : (off == L || off == -(X - 1) * L);
+    return a.lsv[(size_t)a.n_local + (up ? L : 0) + v];
+}
 
 template <typename VT, bool HALO>
 __device__ __forceinline__ double xload(const SpmvK<VT, HALO> &a, int c) {
@@ -587,8 +603,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     }
                     // the row's values do not depend on the column form: issued with the codes
                     // and the dictionary, before the form test waits for the dictionary
+                    if (!a.lsv) {
 #pragma unroll
-                    for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
+                        for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
+                    }
+                }
+                // line-separable values: the row's diagonal, line and position
+                double lsv_d = 0.0;
+                int lsv_x = 0, lsv_v = 0;
+                if (a.lsv) {
+                    lsv_x = (64 * q) / a.lsv_L;
+                    lsv_v = 64 * q - lsv_x * a.lsv_L + lane;
+                    while (lsv_v >= a.lsv_L) {
+                        lsv_v -= a.lsv_L;
+                        ++lsv_x;
+                    }
+                    if (act) lsv_d = __builtin_nontemporal_load(a.lsv + row);
                 }
                 if (a.pk) wide = __shfl(dv, 15, 64) != 0;
                 // one copy of the unrolled entry loop per column form (no branch inside it)
@@ -614,7 +644,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                                 const int off = __shfl(dv, code, 64);
                                 c[u] = code != PK_CODES ? row + off : -1;
                             }
-                            d[u] = (double)dall[k];
+                            d[u] = a.lsv ? (c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0) : (double)dall[k];
                         }
                         batch(c, d, [&] {
                             if constexpr (PIPE) {
@@ -649,6 +679,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 wide = __shfl(dv, 15, 64) != 0;
             }
             const int32_t *cc = a.sell_col + o0 + lane;
+            double lsv_d = 0.0;
+            int lsv_x = 0, lsv_v = 0;
+            if (a.lsv) {
+                lsv_x = (64 * q) / a.lsv_L;
+                lsv_v = 64 * q - lsv_x * a.lsv_L + lane;
+                while (lsv_v >= a.lsv_L) {
+                    lsv_v -= a.lsv_L;
+                    ++lsv_x;
+                }
+                if (act) lsv_d = __builtin_nontemporal_load(a.lsv + row);
+            }
             for (int k0 = 0; k0 < w; k0 += 8) {
                 const uint32_t word = wide ? 0u
                                            : ((VTK_WORD_EARLY && k0 == 0) ? word0
@@ -674,9 +715,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     }
                     // values do not wait for the codes: padding slots hold 0 and are skipped
 #pragma unroll
-                    for (int u = 0; u < PSW; ++u)
-                        d[u] = (VTK_VAL_EARLY ? (h + u < 8 && k0 + h + u < w) : c[u] >= 0)
-                                   ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
+                    for (int u = 0; u < PSW; ++u) {
+                        if (a.lsv) d[u] = c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0;
+                        else d[u] = (VTK_VAL_EARLY ? (h + u < 8 && k0 + h + u < w) : c[u] >= 0)
+                                        ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
+                    }
                     batch(c, d, [] {});
                 }
             }
@@ -981,7 +1024,8 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       sell ? static_cast<const VT *>(in.sell->d_val) : nullptr,
                       sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0,
                       sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
-                      sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0};
+                      sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0,
+                      sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk};
     return a;
 }
 
