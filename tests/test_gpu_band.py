@@ -182,8 +182,16 @@ def test_band_line_separable_values_bit_identical(vk_lib, gpu, name):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     finally:
         del os.environ["VTK_BAND_LSV"]
-    assert s1.band == s0.band == 1 and i1 == i0 == 0 and s1.inner_iters == s0.inner_iters
+    # canonical rows (the kinds' order from the row's line instead of the SELL codes) vs the codes
+    os.environ["VTK_BAND_CANON"] = "0"
+    try:
+        x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+    finally:
+        del os.environ["VTK_BAND_CANON"]
+    assert s1.band == s0.band == s2.band == 1 and i1 == i0 == i2 == 0
+    assert s1.inner_iters == s0.inner_iters == s2.inner_iters
     assert np.array_equal(x1, x0), "line-separable values change the band step's bits"
+    assert np.array_equal(x1, x2), "canonical rows change the band step's bits"
     M.close()
     A.close()
 

@@ -774,6 +774,7 @@ int band_check_all(vtk_csr *A, int64_t L) {
     // reproduce it (f64 values only)
     (void)hipFree(A->d_lsv);
     A->d_lsv = nullptr;
+    A->lsv_canon = false;
     const int64_t n = A->n_local;
     if (!A->fp32 && n % L == 0) {
         const size_t nl = (size_t)n + 2 * (size_t)L + 2 * (size_t)(n / L);
@@ -788,8 +789,12 @@ int band_check_all(vtk_csr *A, int64_t L) {
         int hb = 1;
         HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (hb == 0) A->d_lsv = lsv;
-        else (void)hipFree(lsv);
+        if ((hb & 1) == 0) {
+            A->d_lsv = lsv;
+            A->lsv_canon = (hb & 2) == 0;
+        } else {
+            (void)hipFree(lsv);
+        }
     }
     return VTK_OK;
 }
@@ -921,9 +926,13 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // line-separable values in the band step (VTK_BAND_LSV=0: the SELL values; read per solve)
     const char *lsv_e = std::getenv("VTK_BAND_LSV");
     const bool band_lsv = band && s.A->d_lsv && !(lsv_e && lsv_e[0] == '0');
+    const char *canon_e = std::getenv("VTK_BAND_CANON");   // 0: read the codes anyway (A/B)
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)
-    const double b_band = band_lsv ? b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n : b_csr;
+    const double b_band = band_lsv ? (s.A->lsv_canon && !(canon_e && canon_e[0] == '0')
+                                          ? 8.0 * (double)n   // the diagonal only
+                                          : b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n)
+                                   : b_csr;
     bool broke = false;
     static const int ev_every = [] {
         const char *e = std::getenv("VTK_EV_EVERY");
@@ -1049,6 +1058,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
+            a.canon = band_lsv && s.A->lsv_canon && !(canon_e && canon_e[0] == '0') ? 1 : 0;
             HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));

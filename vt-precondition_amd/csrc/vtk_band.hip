@@ -33,6 +33,37 @@ namespace vtk {
 // (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two workgroups per CU, whose update / SpMV /
 // dots phases overlap.
 // ------------------------------------------------------------------------------------------
+// canonical line-band row (every row of the 2D Vlasov operators): the couplings to lines x - 1
+// (kind 0) and x + 1 (4), to v - 1 (1, absent at v = 0) and v + 1 (3, absent at v = L - 1) and
+// the diagonal (2), stored in ascending column order.  The columns of x -+ 1 in local numbering:
+// one rank periodic ((x -+ 1) mod X) L + v; across ranks the first / last line's outer
+// neighbour is a halo line (n + block L + v).  VM, D, VP are always in that order; the x
+// couplings sort before them ("small") or after them, the two among themselves by column --
+// the same for every v of a line.  Returns the 5 kinds in stored order, 3 bits each.
+__device__ __forceinline__ int canon_order(int64_t r, int64_t n, int L, int X, int lblk, int64_t &cxm, int64_t &cxp) {
+    const int64_t x = r / L, v = r % L;
+    if (lblk < 0) {
+        cxm = ((x - 1 + X) % X) * L + v;
+        cxp = ((x + 1) % X) * L + v;
+    } else {
+        cxm = x >= 1 ? r - L : n + (int64_t)lblk * L + v;
+        cxp = x <= X - 2 ? r + L : n + (int64_t)(1 - lblk) * L + v;
+    }
+    int ord = 0, k = 0;
+    auto put = [&](int kind) { ord |= kind << (3 * k++); };
+    const bool ms = cxm < r, ps = cxp < r;   // "small": before the line's own entries
+    if (ms && ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
+    else if (ms) put(0);
+    else if (ps) put(4);
+    put(1);
+    put(2);
+    put(3);
+    if (!ms && !ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
+    else if (!ms) put(0);
+    else if (!ps) put(4);
+    return ord;
+}
+
 constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
 // geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
 // 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU); the host plans with the GEO 2
@@ -57,10 +88,12 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 #define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
 #endif
 
-// LSV: the matrix values from the line-separable tables (vtk_csr::d_lsv: the diagonal per row,
-// x +- 1 couplings per position v -- held in registers for the lane's v --, v +- 1 couplings per
-// line) instead of the SELL copy's 5 values per row: the same values in the same order
-template <int WU, int J, int GEO, bool LSV = false>
+// VMODE 1 (LSV): the matrix values from the line-separable tables (vtk_csr::d_lsv: the diagonal
+// per row, x +- 1 couplings per position v -- held in registers for the lane's v --, v +- 1
+// couplings per line) instead of the SELL copy's 5 values per row; VMODE 2 (also canonical
+// rows, vtk_csr::lsv_canon): the entries' kinds and order from canon_order instead of the SELL
+// codes and dictionary.  The same values in the same order either way
+template <int WU, int J, int GEO, int VMODE = 0>
 __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
     constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
@@ -83,6 +116,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
     const bool own = tid >= 8 && tid < 8 + LP;
     const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
+    constexpr bool LSV = VMODE >= 1, CANON = VMODE == 2;
     const int ii = lane & 7;
     // LSV: the lane's x-coupling values (position v in every line)
     double tx0 = 0.0, tx1 = 0.0;
@@ -210,9 +244,11 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         double d[LSV ? 1 : WU];
         double mrow = 1.0, drow = 0.0, tv0 = 0.0, tv1 = 0.0;
         if (work) {
-            word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
-            const int64_t qd = q0 + (lane >> 4);
-            dv = (lane < 32 && qd >= 0 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
+            if constexpr (!CANON) {
+                word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
+                const int64_t qd = q0 + (lane >> 4);
+                dv = (lane < 32 && qd >= 0 && qd * 64 < a.n) ? a.dict[qd * 16 + (lane & 15)] : 0;
+            }
             if constexpr (LSV) {
                 if (own) drow = __builtin_nontemporal_load(a.lsv + row);
                 tv0 = a.lsv[a.n + 2 * L + x];
@@ -238,33 +274,59 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         if (work) {
             // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
             double sacc = 0.0, sub = 0.0, sup = 0.0;
-            const int sel = (int)(q - q0) * 16;
+            if constexpr (CANON) {
+                // the line's stored order of the five kinds (the same for every lane of the line)
+                int64_t cxm, cxp;
+                const int ord = __builtin_amdgcn_readfirstlane(
+                    canon_order((int64_t)x * L + (v >= 0 && v < L ? v : 0), a.n, L, X, a.ghost ? a.left_blk : -1, cxm, cxp));
+                const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + 8;   // ring offset of line x
 #pragma unroll
-            for (int k = 0; k < WU; ++k) {
-                const int code = (int)((word >> (4 * k)) & 15u);
-                const int off = __shfl(dv, (sel + code) & 63, 64);
-                if (own && code != PK_CODES) {
-                    // the column's line relative to x and its position in that line, by range
-                    // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
-                    const int t = v + off;
-                    int rel, vc;
-                    const int c = x * L + t;
-                    if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
-                        const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
-                        rel = blk == a.left_blk ? -1 : 1;
-                        vc = kk - blk * L;
-                    } else if (t >= 0 && t < L) { rel = 0; vc = t; }
-                    else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
-                    else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
-                    else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
-                    else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
-                    const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
-                    double dk;
-                    if constexpr (LSV) dk = rel != 0 ? (rel > 0 ? tx1 : tx0) : (vc == v ? drow : (vc > v ? tv1 : tv0));
-                    else dk = d[k];
-                    sacc += dk * xv;
-                    if (off == -1 && ii > 0) sub = sub + dk;
-                    if (off == 1 && ii < 7) sup = sup + dk;
+                for (int e = 0; e < 5; ++e) {
+                    const int kind = (ord >> (3 * e)) & 7;   // uniform
+                    if (own) {
+                        if (kind == 0) sacc += tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + 8 + v];
+                        else if (kind == 4) sacc += tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + 8 + v];
+                        else if (kind == 2) sacc += drow * ring[sx + v];
+                        else if (kind == 1) {
+                            if (v > 0) {
+                                sacc += tv0 * ring[sx + v - 1];
+                                if (ii > 0) sub = sub + tv0;
+                            }
+                        } else if (v < L - 1) {
+                            sacc += tv1 * ring[sx + v + 1];
+                            if (ii < 7) sup = sup + tv1;
+                        }
+                    }
+                }
+            } else {
+                const int sel = (int)(q - q0) * 16;
+#pragma unroll
+                for (int k = 0; k < WU; ++k) {
+                    const int code = (int)((word >> (4 * k)) & 15u);
+                    const int off = __shfl(dv, (sel + code) & 63, 64);
+                    if (own && code != PK_CODES) {
+                        // the column's line relative to x and its position in that line, by range
+                        // tests (vtk_csr_set_line_band checked: lines x-1..x+1, or the periodic wrap)
+                        const int t = v + off;
+                        int rel, vc;
+                        const int c = x * L + t;
+                        if (a.ghost && c >= (int)a.n) {   // halo column: a neighbour rank's line
+                            const int kk = c - (int)a.n, blk = kk >= L ? 1 : 0;
+                            rel = blk == a.left_blk ? -1 : 1;
+                            vc = kk - blk * L;
+                        } else if (t >= 0 && t < L) { rel = 0; vc = t; }
+                        else if (t >= L && t < 2 * L) { rel = 1; vc = t - L; }
+                        else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
+                        else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
+                        else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
+                        const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
+                        double dk;
+                        if constexpr (LSV) dk = rel != 0 ? (rel > 0 ? tx1 : tx0) : (vc == v ? drow : (vc > v ? tv1 : tv0));
+                        else dk = d[k];
+                        sacc += dk * xv;
+                        if (off == -1 && ii > 0) sub = sub + dk;
+                        if (off == 1 && ii < 7) sup = sup + dk;
+                    }
                 }
             }
             const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
@@ -339,7 +401,8 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     switch (a.j) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
-        if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, true>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 1>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         else hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         break;
         VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
@@ -474,6 +537,22 @@ __global__ __launch_bounds__(NT) void k_lsv_build(const int32_t *__restrict__ in
             }
             if (pass == 0) lsv[idx] = data[k];
             else if (__double_as_longlong(lsv[idx]) != __double_as_longlong(data[k])) atomicOr(bad, 1);
+        }
+        if (pass == 1) {
+            // |= 2: the row is not canonical (its stored columns differ from canon_order's)
+            int64_t cxm, cxp;
+            const int ord = canon_order(r, n, L, X, lblk, cxm, cxp);
+            const int64_t v = r % L;
+            int k = indptr[r];
+            bool ok = true;
+            for (int e = 0; e < 5 && ok; ++e) {
+                const int kind = (ord >> (3 * e)) & 7;
+                if ((kind == 1 && v == 0) || (kind == 3 && v == L - 1)) continue;
+                const int64_t c = kind == 0 ? cxm : (kind == 4 ? cxp : r + kind - 2);
+                ok = k < indptr[r + 1] && indices[k] == c;
+                ++k;
+            }
+            if (!ok || k != indptr[r + 1]) atomicOr(bad, 2);
         }
     }
 }

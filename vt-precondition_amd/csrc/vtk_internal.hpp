@@ -182,6 +182,7 @@ struct vtk_csr {
     // when the band is set; the band step then reads 8 B of values per row instead of 40.
     // d_lsv = D | TX | TV; null: not separable (the band step reads the SELL values)
     double *d_lsv = nullptr;
+    bool lsv_canon = false;   // ... and every row canonical (canon_order): the band step reads no codes
     // distributed band step: the halo is two neighbour lines; peers and the alltoallv layout of
     // the per-step ghost exchange (BAND_GHOST_VECS L doubles per side), -1 offsets: no such side
     bool band_ghost = false;                            // band across ranks: per-step ghost exchange
@@ -385,6 +386,7 @@ struct BandK {
                                  // (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
     const double *lsv;           // line-separable values (vtk_csr::d_lsv) or null: SELL values
+    int canon;                   // with lsv: canonical rows (vtk_csr::lsv_canon), no codes read
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
 // geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
