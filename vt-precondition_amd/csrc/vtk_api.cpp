@@ -328,8 +328,8 @@ bool bj_fused(const vtk_prec *M) {
 // has them: the same values, the same sums, 8 B of values per row instead of 40 (VTK_BAND_LSV=0:
 // the SELL values; read per call).  vtk_spmv keeps the SELL values: it is the measured SpMV
 bool lsv_on(const vtk_csr *A) {
-    const char *e = std::getenv("VTK_BAND_LSV");
-    return A->use_sell && A->d_lsv && A->band_L > 0 && !A->fp32 && !(e && e[0] == '0') &&
+    const char *e = std::getenv("VTK_BAND_LSV"), *e2 = std::getenv("VTK_SELL_LSV");
+    return A->use_sell && A->d_lsv && A->band_L > 0 && !A->fp32 && !(e && e[0] == '0') && !(e2 && e2[0] == '0') &&
            (!A->ctx->dist || A->band_ghost);
 }
 SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
