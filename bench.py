@@ -419,7 +419,9 @@ def main():
     csr_matrix_bytes = (4 if fp32 else 8) * nnz_loc + 4 * nnz_loc + 4 * (n_loc + 1)
     # the band step reads the SELL codes and -- line-separable operators (A.line_separable) --
     # 8 B of values per row from the diagonal table instead of the SELL values (vtk_api.cpp b_band)
-    band_matrix = linfo["matrix_bytes"] - (8.0 * linfo["sell_entries"] - 8.0 * n_loc if A.line_separable else 0.0)
+    lv = A.line_values   # 2: canonical rows, the band step reads only the diagonal table
+    band_matrix = 8.0 * n_loc if lv == 2 else \
+        linfo["matrix_bytes"] - (8.0 * linfo["sell_entries"] - 8.0 * n_loc if lv == 1 else 0.0)
     d_matrix = csr_matrix_bytes - (band_matrix if dom == "band_step" else linfo["matrix_bytes"])
     dom_csr = dk["bytes"] / dk["launches"] + (d_matrix if dom.startswith("spmv") or dom == "band_step" else 0.0)
     solve_bytes = sum(v["bytes"] for v in kprof.values())
@@ -522,7 +524,7 @@ def main():
         dist.destroy_process_group()
 
 
-KERNEL_SOURCES = ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp")
+KERNEL_SOURCES = ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp", "vtk_scalar.hpp")
 
 
 def kernels_sha16():

@@ -220,7 +220,10 @@ int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len);
  * the same line only on the line x (the 2D Vlasov operators: advection in x with speed v, force
  * along v with field E(x)).  Checked bit for bit against the CSR when the band is set; the band
  * step then reads the diagonal per row and those couplings from per-position / per-line tables
- * (8 B of values per row instead of 40; the same values, summed in the same order).  ABI 4. */
+ * (8 B of values per row instead of 40; the same values, summed in the same order).  2: also
+ * every row canonical (the couplings to x-1, v-1, the diagonal, v+1, x+1 in ascending column
+ * order): the band step derives the entries' kinds and order from the row's line and reads no
+ * column codes either.  ABI 4. */
 int vtk_csr_get_line_values(vtk_csr *A, int *separable);
 
 /* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged

@@ -112,7 +112,7 @@ def main():
     fetch = load(os.path.join(src, a.fetch, "run_counter_collection.csv"))
     write = load(os.path.join(src, a.write, "run_counter_collection.csv"))
     hsh = hashlib.sha256()   # the device sources, in bench.py's KERNEL_SOURCES order
-    for name in ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp"):
+    for name in ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp", "vtk_scalar.hpp"):
         with open(os.path.join(root, "vt-precondition_amd", "csrc", name), "rb") as f:
             hsh.update(f.read())
     ksha = hsh.hexdigest()[:16]

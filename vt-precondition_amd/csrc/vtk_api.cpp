@@ -1962,7 +1962,7 @@ int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len) {
 
 int vtk_csr_get_line_values(vtk_csr *A, int *separable) {
     if (!A || !separable) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_csr_get_line_values: NULL argument");
-    *separable = A->band_L > 0 && A->d_lsv != nullptr ? 1 : 0;
+    *separable = A->band_L > 0 && A->d_lsv != nullptr ? (A->lsv_canon ? 2 : 1) : 0;
     return VTK_OK;
 }
 

@@ -233,9 +233,15 @@ class CsrOperator:
         """True when the band step reads the values from per-position / per-line tables (the
         operator's x couplings depend only on v, its v couplings only on x; checked bit for bit
         when the band was set -- vtk_csr_get_line_values)."""
+        return self.line_values > 0
+
+    @property
+    def line_values(self) -> int:
+        """0: SELL values; 1: line-separable values; 2: also canonical rows (no column codes read
+        by the band step) -- vtk_csr_get_line_values."""
         v = C.c_int()
         check(lib().vtk_csr_get_line_values(self._h, C.byref(v)), self.ctx.handle)
-        return bool(v.value)
+        return v.value
 
     def layout_info(self) -> dict:
         """Layout in use, bytes of the operator one SpMV reads in it, SELL chunk counts."""
