@@ -606,7 +606,7 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
                 if (off == 0) val = drow;
                 else if (off == 1 || off == -1) val = lsv[(size_t)n + 2 * L + (off > 0 ? X : 0) + xl];
                 else {
-                    const bool up = (HALO && c >= n) ? ((c - n) / L != lblk) : (off == L || off == -(X - 1) * L);
+                    const bool up = (HALO && c >= n) ? ((c - n) / L != lblk) : (off == L || (lblk < 0 && off == -(X - 1) * L));
                     val = lsv[(size_t)n + (up ? L : 0) + v];
                 }
                 const double xv = (HALO && c >= n) ? halo[c - n] : x[c];

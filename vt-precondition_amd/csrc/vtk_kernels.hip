@@ -73,7 +73,10 @@ __device__ __forceinline__ double lsv_value(const SpmvK<VT, HALO> &a, int row, i
     const int off = c - row, L = a.lsv_L, X = a.n_local / L;
     if (off == 0) return drow;
     if (off == 1 || off == -1) return a.lsv[(size_t)a.n_local + 2 * L + (off > 0 ? X : 0) + xl];
-    const bool up = (HALO && c >= a.n_local) ? ((c - a.n_local) / L != a.lsv_lblk) : (off == L || off == -(X - 1) * L);
+    // the periodic wrap only on one rank (lblk < 0): across ranks a slab of two lines has
+    // -(X - 1) L == -L, the x - 1 coupling
+    const bool up = (HALO && c >= a.n_local) ? ((c - a.n_local) / L != a.lsv_lblk)
+                                             : (off == L || (a.lsv_lblk < 0 && off == -(X - 1) * L));
     return a.lsv[(size_t)a.n_local + (up ? L : 0) + v];
 }
 
