@@ -188,10 +188,18 @@ def test_band_line_separable_values_bit_identical(vk_lib, gpu, name):
         x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     finally:
         del os.environ["VTK_BAND_CANON"]
-    assert s1.band == s0.band == s2.band == 1 and i1 == i0 == i2 == 0
-    assert s1.inner_iters == s0.inner_iters == s2.inner_iters
+    # the cycle-start SELL launches (residual + BJ, step 0's SpMV + BJ + dots) with their columns
+    # from canon_row vs the codes
+    os.environ["VTK_SELL_CANON"] = "0"
+    try:
+        x3, i3, s3 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+    finally:
+        del os.environ["VTK_SELL_CANON"]
+    assert s1.band == s0.band == s2.band == s3.band == 1 and i1 == i0 == i2 == i3 == 0
+    assert s1.inner_iters == s0.inner_iters == s2.inner_iters == s3.inner_iters
     assert np.array_equal(x1, x0), "line-separable values change the band step's bits"
     assert np.array_equal(x1, x2), "canonical rows change the band step's bits"
+    assert np.array_equal(x1, x3), "canonical rows change the SELL launches' bits"
     M.close()
     A.close()
 
@@ -237,7 +245,14 @@ def test_separable_values_in_unfused_paths_bit_identical(vk_lib, gpu, orth):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
     finally:
         del os.environ["VTK_BAND_LSV"]
-    assert s1.band == s0.band == 0 and i1 == i0 == 0 and s1.inner_iters == s0.inner_iters
+    os.environ["VTK_SELL_CANON"] = "0"   # the SELL codes instead of canon_row's columns
+    try:
+        x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
+    finally:
+        del os.environ["VTK_SELL_CANON"]
+    assert s1.band == s0.band == s2.band == 0 and i1 == i0 == i2 == 0
+    assert s1.inner_iters == s0.inner_iters == s2.inner_iters
     assert np.array_equal(x1, x0)
+    assert np.array_equal(x1, x2)
     M.close()
     A.close()

@@ -318,5 +318,12 @@ def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
         del os.environ["VTK_BAND_LSV"]
     assert i1 == i0 == 0 and it1 == vk_lib.last_stats().inner_iters
     assert np.array_equal(x1, x0)
+    os.environ["VTK_SELL_CANON"] = "0"   # the SELL codes instead of canon_row's columns
+    try:
+        x2, i2 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
+    finally:
+        del os.environ["VTK_SELL_CANON"]
+    assert i2 == 0 and it1 == vk_lib.last_stats().inner_iters
+    assert np.array_equal(x1, x2)
     M.close()
     A.close()

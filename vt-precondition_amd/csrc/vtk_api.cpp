@@ -337,6 +337,9 @@ SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
         in.lsv = A->d_lsv;
         in.lsv_L = (int)A->band_L;
         in.lsv_lblk = A->band_ghost ? A->band_lblk : -1;
+        // VTK_SELL_CANON=0 (A/B, read per launch): the SELL codes even for canonical rows
+        const char *e = std::getenv("VTK_SELL_CANON");
+        in.lsv_canon = A->lsv_canon && !(e && e[0] == '0') ? 1 : 0;
     }
     return in;
 }
@@ -344,7 +347,10 @@ double matrix_bytes(const vtk_csr *A);
 // matrix bytes a solver SELL launch reads (lsv_in)
 double solver_matrix_bytes(const vtk_csr *A) {
     const double b = matrix_bytes(A);
-    return lsv_on(A) ? b - 8.0 * (double)A->sell.entries + 8.0 * (double)A->n_local : b;
+    if (!lsv_on(A)) return b;
+    const char *e = std::getenv("VTK_SELL_CANON");
+    if (A->lsv_canon && !(e && e[0] == '0')) return 8.0 * (double)A->n_local;   // the diagonal only
+    return b - 8.0 * (double)A->sell.entries + 8.0 * (double)A->n_local;
 }
 
 // interior / boundary pieces of the fused SpMV (world > 1)
@@ -893,6 +899,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = matrix_bytes(s.A);
     const double b_lsv = b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n;
+    // canonical rows: the diagonal only (VTK_SELL_CANON=0: the codes too; A/B)
+    const char *canon_l = std::getenv("VTK_SELL_CANON");
+    const bool line_canon = line_lsv && s.A->lsv_canon && !(canon_l && canon_l[0] == '0');
     const double b_inv = bj_row_bytes(s.M) * n;
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
     // (folding the finalize into the boundary launch's last workgroup was measured slower: one
@@ -987,10 +996,10 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             TRY(halo_exchange(s.A, pj));
             if (line_lsv) {
                 // line-separable values: 12 B of matrix per row (codes + diagonal)
-                Prof pf(c, "spmv_lsv", j, b_lsv + 2 * n8);
+                Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
                                           s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
-                                          c->stream));
+                                          c->stream, line_canon ? 1 : 0));
             } else {
                 Prof pf(c, "spmv", j, b_csr + 2 * n8);
                 HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,

@@ -33,36 +33,7 @@ namespace vtk {
 // (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two workgroups per CU, whose update / SpMV /
 // dots phases overlap.
 // ------------------------------------------------------------------------------------------
-// canonical line-band row (every row of the 2D Vlasov operators): the couplings to lines x - 1
-// (kind 0) and x + 1 (4), to v - 1 (1, absent at v = 0) and v + 1 (3, absent at v = L - 1) and
-// the diagonal (2), stored in ascending column order.  The columns of x -+ 1 in local numbering:
-// one rank periodic ((x -+ 1) mod X) L + v; across ranks the first / last line's outer
-// neighbour is a halo line (n + block L + v).  VM, D, VP are always in that order; the x
-// couplings sort before them ("small") or after them, the two among themselves by column --
-// the same for every v of a line.  Returns the 5 kinds in stored order, 3 bits each.
-__device__ __forceinline__ int canon_order(int64_t r, int64_t n, int L, int X, int lblk, int64_t &cxm, int64_t &cxp) {
-    const int64_t x = r / L, v = r % L;
-    if (lblk < 0) {
-        cxm = ((x - 1 + X) % X) * L + v;
-        cxp = ((x + 1) % X) * L + v;
-    } else {
-        cxm = x >= 1 ? r - L : n + (int64_t)lblk * L + v;
-        cxp = x <= X - 2 ? r + L : n + (int64_t)(1 - lblk) * L + v;
-    }
-    int ord = 0, k = 0;
-    auto put = [&](int kind) { ord |= kind << (3 * k++); };
-    const bool ms = cxm < r, ps = cxp < r;   // "small": before the line's own entries
-    if (ms && ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
-    else if (ms) put(0);
-    else if (ps) put(4);
-    put(1);
-    put(2);
-    put(3);
-    if (!ms && !ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
-    else if (!ms) put(0);
-    else if (!ps) put(4);
-    return ord;
-}
+// canonical line-band rows: canon_order (vtk_device.hpp)
 
 constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
 // geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
@@ -278,7 +249,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                 // the line's stored order of the five kinds (the same for every lane of the line)
                 int64_t cxm, cxp;
                 const int ord = __builtin_amdgcn_readfirstlane(
-                    canon_order((int64_t)x * L + (v >= 0 && v < L ? v : 0), a.n, L, X, a.ghost ? a.left_blk : -1, cxm, cxp));
+                    canon_order_xv(x, 0, a.n, L, X, a.ghost ? a.left_blk : -1, cxm, cxp));
                 const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + 8;   // ring offset of line x
 #pragma unroll
                 for (int e = 0; e < 5; ++e) {
@@ -575,7 +546,9 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
 // row): k_sell's plain SpMV -- entries in stored order, padding skipped -- reading 12 B of
 // matrix per row instead of 44.  lblk < 0: one rank (x couplings periodic); else the halo
 // block of the left neighbour line (HALO: the halo columns read from halo[])
-template <bool HALO>
+// CANON (every row canonical, vtk_csr::lsv_canon): the columns and values from canon_row -- no
+// code word or dictionary loaded, the gathers issue with the diagonal
+template <bool HALO, bool CANON = false>
 __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk, const int32_t *__restrict__ dict,
                                                  const double *__restrict__ lsv, const double *__restrict__ x,
                                                  const double *__restrict__ halo, double *__restrict__ y, int n, int L,
@@ -586,8 +559,6 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
     for (int q = (int)(((int64_t)blockIdx.x * NT + threadIdx.x) >> 6); q < nch; q += (int)((int64_t)gridDim.x * NT >> 6)) {
         const int r = 64 * q + lane;
         const bool act = r < n;
-        const uint32_t word = act ? __builtin_nontemporal_load(pk + (size_t)q * 64 + lane) : ~0u;
-        const int dv = lane < 16 ? dict[(size_t)q * 16 + lane] : 0;
         // the row's line and position: the chunk's first row by one division, then the lane
         int xl = (64 * q) / L, v = 64 * q - xl * L + lane;
         while (v >= L) {
@@ -596,6 +567,26 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
         }
         const double drow = act ? __builtin_nontemporal_load(lsv + r) : 0.0;
         double s = 0.0;
+        if constexpr (CANON) {
+            if (act) {
+                int c[5];
+                double d[5];
+                canon_row(lsv, n, L, lblk, xl, v, drow, c, d);
+                double xv[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    const int cc = c[k] >= 0 ? c[k] : r;
+                    xv[k] = (HALO && cc >= n) ? halo[cc - n] : x[cc];
+                }
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    if (c[k] >= 0) s += d[k] * xv[k];
+                __builtin_nontemporal_store(s, y + r);
+            }
+            continue;
+        }
+        const uint32_t word = act ? __builtin_nontemporal_load(pk + (size_t)q * 64 + lane) : ~0u;
+        const int dv = lane < 16 ? dict[(size_t)q * 16 + lane] : 0;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const int code = (int)((word >> (4 * k)) & 15u);
@@ -619,11 +610,13 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
 
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s) {
+                           hipStream_t s, int canon) {
     if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || (halo && lblk < 0)) return hipErrorInvalidValue;
     const int64_t nch = (n + 63) / 64;
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>((nch + 3) / 4, 2048));
-    if (halo) hipLaunchKernelGGL(k_lsv_spmv<true>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
+    if (canon && halo) hipLaunchKernelGGL((k_lsv_spmv<true, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
+    else if (canon) hipLaunchKernelGGL((k_lsv_spmv<false, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
+    else if (halo) hipLaunchKernelGGL(k_lsv_spmv<true>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
     else hipLaunchKernelGGL(k_lsv_spmv<false>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
     return hipGetLastError();
 }

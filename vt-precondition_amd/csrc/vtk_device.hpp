@@ -11,6 +11,62 @@
 
 namespace vtk {
 
+// canonical line-band row (every row of the 2D Vlasov operators): the couplings to lines x - 1
+// (kind 0) and x + 1 (4), to v - 1 (1, absent at v = 0) and v + 1 (3, absent at v = L - 1) and
+// the diagonal (2), stored in ascending column order.  The columns of x -+ 1 in local numbering:
+// one rank periodic ((x -+ 1) mod X) L + v; across ranks the first / last line's outer
+// neighbour is a halo line (n + block L + v).  VM, D, VP are always in that order; the x
+// couplings sort before them ("small") or after them, the two among themselves by column --
+// the same for every v of a line.  Returns the 5 kinds in stored order, 3 bits each.
+__device__ __forceinline__ int canon_order_xv(int64_t x, int64_t v, int64_t n, int L, int X, int lblk, int64_t &cxm,
+                                              int64_t &cxp) {
+    const int64_t r = x * L + v;
+    if (lblk < 0) {
+        cxm = ((x - 1 + X) % X) * L + v;
+        cxp = ((x + 1) % X) * L + v;
+    } else {
+        cxm = x >= 1 ? r - L : n + (int64_t)lblk * L + v;
+        cxp = x <= X - 2 ? r + L : n + (int64_t)(1 - lblk) * L + v;
+    }
+    int ord = 0, k = 0;
+    auto put = [&](int kind) { ord |= kind << (3 * k++); };
+    const bool ms = cxm < r, ps = cxp < r;   // "small": before the line's own entries
+    if (ms && ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
+    else if (ms) put(0);
+    else if (ps) put(4);
+    put(1);
+    put(2);
+    put(3);
+    if (!ms && !ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
+    else if (!ms) put(0);
+    else if (!ps) put(4);
+    return ord;
+}
+__device__ __forceinline__ int canon_order(int64_t r, int64_t n, int L, int X, int lblk, int64_t &cxm, int64_t &cxp) {
+    return canon_order_xv(r / L, r % L, n, L, X, lblk, cxm, cxp);
+}
+
+// the entries of canonical row (xl, v) -- row = xl L + v, local numbering, n local rows, X = n / L
+// lines -- in stored order from the line-separable tables lsv = D[n] | TX[2][L] | TV[2][X]
+// (vtk_band.hip k_lsv_build): column c[e] (-1: kind absent at v = 0 / L - 1) and value d[e].
+// The SELL copy of the same row holds the same columns and values in the same order, padding
+// after them, so a sum over these in order equals the SELL sum bit for bit
+__device__ __forceinline__ void canon_row(const double *__restrict__ lsv, int n, int L, int lblk, int xl, int v,
+                                          double drow, int (&c)[5], double (&d)[5]) {
+    const int X = n / L, row = xl * L + v;
+    int64_t cxm, cxp;
+    const int ord = canon_order_xv(xl, v, n, L, X, lblk, cxm, cxp);
+#pragma unroll
+    for (int e = 0; e < 5; ++e) {
+        const int kind = (ord >> (3 * e)) & 7;
+        if (kind == 0) { c[e] = (int)cxm; d[e] = lsv[(size_t)n + v]; }
+        else if (kind == 4) { c[e] = (int)cxp; d[e] = lsv[(size_t)n + L + v]; }
+        else if (kind == 2) { c[e] = row; d[e] = drow; }
+        else if (kind == 1) { c[e] = v > 0 ? row - 1 : -1; d[e] = v > 0 ? lsv[(size_t)n + 2 * L + xl] : 0.0; }
+        else { c[e] = v < L - 1 ? row + 1 : -1; d[e] = v < L - 1 ? lsv[(size_t)n + 2 * L + X + xl] : 0.0; }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // reductions
 // ------------------------------------------------------------------------------------------

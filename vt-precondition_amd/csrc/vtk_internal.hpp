@@ -230,6 +230,7 @@ struct SpmvIn {
     // line-separable values (SELL, f64; solver launches only -- vtk_spmv keeps the SELL values)
     const double *lsv = nullptr;
     int lsv_L = 0, lsv_lblk = -1;
+    int lsv_canon = 0;   // ... and every row canonical: k_sell computes the columns (canon_row)
 };
 
 LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);
@@ -412,7 +413,7 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
 // k_sell's plain SpMV, the same bits.  halo != null: the distributed layout (lblk the left block)
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s);
+                           hipStream_t s, int canon = 0);   // canon: rows canonical, no codes read
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 

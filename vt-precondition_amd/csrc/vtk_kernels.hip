@@ -64,6 +64,7 @@ struct SpmvK {
     // entry's value from its column -- the same value, so the same sums
     const double *lsv;
     int lsv_L, lsv_lblk;
+    int canon;   // with lsv: every row canonical (vtk_csr::lsv_canon): columns from canon_row
 };
 
 // value of entry (row, c) from the line-separable tables; drow = D[row], (xl, v) the row's line
@@ -582,7 +583,33 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 }
             }
         };
-        if constexpr (WU > 0) {
+        // canonical line-band rows with line-separable values (a.canon): every entry's column
+        // and value from the row's line and position -- no code words, dictionary or values
+        // loaded, so the gathers issue with the row's diagonal instead of after two dependent
+        // round trips; the same entries in the same order as the SELL copy (canon_row)
+        constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE;
+        if (CANON_OK && a.canon) {
+            if (64 * q < a.n_local) {
+                const int L = a.lsv_L;
+                int xl = (64 * q) / L, v = 64 * q - xl * L + lane;
+                while (v >= L) {
+                    v -= L;
+                    ++xl;
+                }
+                int c[5];
+                double d[5];
+                if (act) {
+                    canon_row(a.lsv, a.n_local, L, a.lsv_lblk, xl, v, __builtin_nontemporal_load(a.lsv + row), c, d);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 5; ++u) {
+                        c[u] = -1;
+                        d[u] = 0.0;
+                    }
+                }
+                batch(c, d, [] {});
+            }
+        } else if constexpr (WU > 0) {
             if (64 * q < a.n_local) {
                 constexpr int NWD = (WU + 7) / 8;   // 4-bit code words per lane
                 const int64_t o0 = (int64_t)q * 64 * WU;
@@ -1028,7 +1055,8 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0,
                       sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
                       sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0,
-                      sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk};
+                      sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk,
+                      sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0};
     return a;
 }
 
