@@ -21,9 +21,9 @@ namespace vtk {
 __device__ __forceinline__ int canon_order_xv(int64_t x, int64_t v, int64_t n, int L, int X, int lblk, int64_t &cxm,
                                               int64_t &cxp) {
     const int64_t r = x * L + v;
-    if (lblk < 0) {
-        cxm = ((x - 1 + X) % X) * L + v;
-        cxp = ((x + 1) % X) * L + v;
+    if (lblk < 0) {   // (x -+ 1) mod X for 0 <= x < X, by selects (no 64-bit division)
+        cxm = (x == 0 ? X - 1 : x - 1) * L + v;
+        cxp = (x == X - 1 ? 0 : x + 1) * L + v;
     } else {
         cxm = x >= 1 ? r - L : n + (int64_t)lblk * L + v;
         cxp = x <= X - 2 ? r + L : n + (int64_t)(1 - lblk) * L + v;
@@ -65,6 +65,17 @@ __device__ __forceinline__ void canon_row(const double *__restrict__ lsv, int n,
         else if (kind == 1) { c[e] = v > 0 ? row - 1 : -1; d[e] = v > 0 ? lsv[(size_t)n + 2 * L + xl] : 0.0; }
         else { c[e] = v < L - 1 ? row + 1 : -1; d[e] = v < L - 1 ? lsv[(size_t)n + 2 * L + X + xl] : 0.0; }
     }
+}
+
+// Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
+// 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
+// contiguous id range; with the grid-stride tile loop an XCD then works on a contiguous window
+// of tiles at a time and neighbouring tiles' x halos (+-nv rows on the 2D operator) hit its L2.
+// Speed only: the partial of workgroup b stays at index b, every mapping is fixed.
+__device__ __forceinline__ int xcd_swizzle(int b, int g) {
+    constexpr int NX = 8;
+    const int q = g / NX, r = g % NX, x = b % NX;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / NX;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -104,17 +104,6 @@ __device__ __forceinline__ void load_inv_row(const double *irow, double (&m)[BS]
 }
 
 
-// Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
-// 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
-// contiguous id range; with the grid-stride tile loop an XCD then works on a contiguous window
-// of tiles at a time and neighbouring tiles' x halos (+-nv rows on the 2D operator) hit its L2.
-// Speed only: the partial of workgroup b stays at index b, every mapping is fixed.
-__device__ __forceinline__ int xcd_swizzle(int b, int g) {
-    constexpr int NX = 8;
-    const int q = g / NX, r = g % NX, x = b % NX;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / NX;
-}
-
 // DCGS2 dots of rows [i0, i1) of a tile, w and p staged in LDS (wt, pt): wave wv owns the basis
 // vectors k = wv, wv + 4, ...; W = 2: 16-byte loads of V (the tile's first row even)
 constexpr int DC_KPW = DC_MAXJ / (NT / 64);
