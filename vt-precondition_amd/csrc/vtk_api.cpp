@@ -936,6 +936,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const char *lsv_e = std::getenv("VTK_BAND_LSV");
     const bool band_lsv = band && s.A->d_lsv && !(lsv_e && lsv_e[0] == '0');
     const char *canon_e = std::getenv("VTK_BAND_CANON");   // 0: read the codes anyway (A/B)
+    const char *canon_sl_e = std::getenv("VTK_BAND_CANON_SL");   // 0: the per-entry loop (A/B)
+    const bool canon_sl = !(canon_sl_e && canon_sl_e[0] == '0');
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)
     const double b_band = band_lsv ? (s.A->lsv_canon && !(canon_e && canon_e[0] == '0')
@@ -1067,7 +1069,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
-            a.canon = band_lsv && s.A->lsv_canon && !(canon_e && canon_e[0] == '0') ? 1 : 0;
+            a.canon = band_lsv && s.A->lsv_canon && !(canon_e && canon_e[0] == '0') ? (canon_sl ? 2 : 1) : 0;
             HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));

@@ -251,10 +251,50 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                 const int ord = __builtin_amdgcn_readfirstlane(
                     canon_order_xv(x, 0, a.n, L, X, a.ghost ? a.left_blk : -1, cxm, cxp));
                 const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + 8;   // ring offset of line x
+                // the three orders the lines take (interior / first line / last line of one rank),
+                // straight-line: every lane reads its five operands (a clamped row off its own
+                // rows), the absent v -+ 1 terms are skipped by selects -- the same additions in
+                // the same order as the loop below, without its per-entry exec-mask branches
+                constexpr int P_MID = 0 | 1 << 3 | 2 << 6 | 3 << 9 | 4 << 12;
+                constexpr int P_FIRST = 1 | 2 << 3 | 3 << 6 | 4 << 9 | 0 << 12;
+                constexpr int P_LAST = 4 | 0 << 3 | 1 << 6 | 2 << 9 | 3 << 12;
+                const bool sl = a.canon == 2 && (ord == P_MID || ord == P_FIRST || ord == P_LAST);   // uniform
+                if (sl) {
+                    const int vv = own ? v : v0;
+                    const double t0 = tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + 8 + vv];
+                    const double t4 = tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + 8 + vv];
+                    const double t2 = drow * ring[sx + vv];
+                    const double t1 = tv0 * ring[sx + vv - 1];
+                    const double t3 = tv1 * ring[sx + vv + 1];
+                    const bool h1 = vv > 0, h3 = vv < L - 1;
+                    double sa = 0.0;
+                    if (ord == P_MID) {
+                        sa = sa + t0;
+                        sa = h1 ? sa + t1 : sa;
+                        sa = sa + t2;
+                        sa = h3 ? sa + t3 : sa;
+                        sa = sa + t4;
+                    } else if (ord == P_FIRST) {
+                        sa = h1 ? sa + t1 : sa;
+                        sa = sa + t2;
+                        sa = h3 ? sa + t3 : sa;
+                        sa = sa + t4;
+                        sa = sa + t0;
+                    } else {
+                        sa = sa + t4;
+                        sa = sa + t0;
+                        sa = h1 ? sa + t1 : sa;
+                        sa = sa + t2;
+                        sa = h3 ? sa + t3 : sa;
+                    }
+                    sacc = own ? sa : 0.0;
+                    sub = (own && h1 && ii > 0) ? 0.0 + tv0 : 0.0;
+                    sup = (own && h3 && ii < 7) ? 0.0 + tv1 : 0.0;
+                }
 #pragma unroll
                 for (int e = 0; e < 5; ++e) {
                     const int kind = (ord >> (3 * e)) & 7;   // uniform
-                    if (own) {
+                    if (!sl && own) {
                         if (kind == 0) sacc += tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + 8 + v];
                         else if (kind == 4) sacc += tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + 8 + v];
                         else if (kind == 2) sacc += drow * ring[sx + v];

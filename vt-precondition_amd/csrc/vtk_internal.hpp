@@ -387,7 +387,8 @@ struct BandK {
                                  // (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
     const double *lsv;           // line-separable values (vtk_csr::d_lsv) or null: SELL values
-    int canon;                   // with lsv: canonical rows (vtk_csr::lsv_canon), no codes read
+    int canon;                   // with lsv: canonical rows (vtk_csr::lsv_canon), no codes read;
+                                 // 2: the SpMV as straight-line code per line order
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
 // geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
