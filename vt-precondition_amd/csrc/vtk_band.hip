@@ -55,6 +55,10 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 #ifndef VTK_BAND_PF
 #define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 8)   // j <= this: next line's update operands prefetched across SpMV + dots
 #endif
+#ifndef VTK_BAND_GHT
+#define VTK_BAND_GHT 1   // one rank (no ghost lines): the instantiation without the ghost paths
+                         // (band step 563-569 vs 571-575 us, process A/B 3 reps)
+#endif
 #ifndef VTK_BAND_VBUF_FIXED
 #define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
 #endif
@@ -64,7 +68,7 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 // couplings per line) instead of the SELL copy's 5 values per row; VMODE 2 (also canonical
 // rows, vtk_csr::lsv_canon): the entries' kinds and order from canon_order instead of the SELL
 // codes and dictionary.  The same values in the same order either way
-template <int WU, int J, int GEO, int VMODE = 0>
+template <int WU, int J, int GEO, int VMODE = 0, bool GH = true>
 __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
     constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         // a rank's first / last line range: the x-halo line is a neighbour rank's line, whose
         // V_k (k < j), w_j and w_{j-1} arrived in the ghost buffer (slots k, m + (j & 1),
         // m + ((j - 1) & 1); v_0 in slot 0 at j = 0)
-        const double *gh = (a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
+        const double *gh = (GH && a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1)))
                                ? a.ghost + (size_t)(kind == 1 ? 0 : 1) * (a.m + 2) * L : nullptr;
         if (upd) {
             if (gh) {
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
                 // the line's stored order of the five kinds (the same for every lane of the line)
                 int64_t cxm, cxp;
                 const int ord = __builtin_amdgcn_readfirstlane(
-                    canon_order_xv(x, 0, a.n, L, X, a.ghost ? a.left_blk : -1, cxm, cxp));
+                    canon_order_xv(x, 0, a.n, L, X, GH && a.ghost ? a.left_blk : -1, cxm, cxp));
                 const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + 8;   // ring offset of line x
                 // the three orders the lines take (interior / first line / last line of one rank),
                 // straight-line: every lane reads its five operands (a clamped row off its own
@@ -412,7 +416,8 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     switch (a.j) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
-        if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        if (a.lsv && a.canon && VTK_BAND_GHT && !a.ghost) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2, false>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        else if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 1>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         else hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         break;
