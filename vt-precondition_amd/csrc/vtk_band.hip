@@ -115,9 +115,10 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     // line of iteration it (it = 0: the x-halo line before xa; it = nl + 1: the one after xb - 1;
     // kind 1 / 2, recomputed, nothing stored)
     const int nl = xb - xa;
+    const int xhm = xa == 0 ? X - 1 : xa - 1, xhp = xb == X ? 0 : xb;   // the x-halo lines (mod X)
     auto line_of = [&](int it, int &kind) {
         kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
-        return it == 0 ? (xa - 1 + X) % X : (it == nl + 1 ? xb % X : xa - 1 + it);
+        return it == 0 ? xhm : (it == nl + 1 ? xhp : xa - 1 + it);
     };
     // software pipeline (J <= VTK_BAND_PF, as the registers allow): the next line's update
     // operands are loaded during this line's SpMV and dots.  (A partial prefetch of 4 basis rows
@@ -153,10 +154,13 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
             for (int k = 0; k < J; ++k) o.v[k] = upd ? gh[(size_t)k * L + v] : 0.0;
         } else {
+            // one lane pointer stepped by ld (per-k scalar bases would spill SGPRs: readlanes)
+            const double *pv = a.V + row;
 #pragma unroll
-            for (int k = 0; k < J; ++k)
-                o.v[k] = upd ? (VTK_BAND_REREAD ? a.V[(size_t)k * a.ld + row]
-                                                : __builtin_nontemporal_load(a.V + (size_t)k * a.ld + row)) : 0.0;
+            for (int k = 0; k < J; ++k) {
+                o.v[k] = upd ? (VTK_BAND_REREAD ? *pv : __builtin_nontemporal_load(pv)) : 0.0;
+                pv += a.ld;
+            }
         }
     };
     // the update itself: p_j as step j-1's update formed it, then k_dc_update's operations;
