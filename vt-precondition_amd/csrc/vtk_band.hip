@@ -53,7 +53,8 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 #define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
 #endif
 #ifndef VTK_BAND_PF
-#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 8)   // j <= this: next line's update operands prefetched across SpMV + dots
+#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 10)   // j <= this: next line's update operands prefetched across SpMV + dots
+                                                 // (10: 567-570 us; 8: 570; 12: 567; 18: 624, spills)
 #endif
 #ifndef VTK_BAND_GHT
 #define VTK_BAND_GHT 1   // one rank (no ghost lines): the instantiation without the ghost paths
