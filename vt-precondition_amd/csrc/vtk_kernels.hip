@@ -576,7 +576,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // and value from the row's line and position -- no code words, dictionary or values
         // loaded, so the gathers issue with the row's diagonal instead of after two dependent
         // round trips; the same entries in the same order as the SELL copy (canon_row)
-        constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE;
+        // (not in the plain SpMV: vtk_spmv, the measured standalone SpMV, never has lsv, and the
+        // extra path cost its loop 249 -> 372 us on C3 through code shape alone)
+        constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE && EPI != EPI_PLAIN;
         if (CANON_OK && a.canon) {
             if (64 * q < a.n_local) {
                 const int L = a.lsv_L;
