@@ -190,6 +190,10 @@ def main():
                     help="preconditioner: bj (block-Jacobi(bs), SURVEY §8d, the metric's config) or line "
                          "(line-Jacobi along x, segments of --seg x-points, SURVEY §8f-4)")
     ap.add_argument("--seg", type=int, default=25, help="line-Jacobi segment length (x-points)")
+    ap.add_argument("--operator", default="generated", choices=["generated", "upload", "npz"],
+                    help="generated: assembled on the device (vtk_csr_create_vlasov); upload: the same "
+                         "CSR handed over as host arrays (vtkrylov.csr_matrix, the drop-in path); npz: "
+                         "written with save_npz and read back with vtkrylov.load_npz")
     ap.add_argument("--comm-solo", action="store_true",
                     help="one GPU through the distributed code paths (one-rank RCCL communicator)")
     ap.add_argument("--slab", type=int, default=1,
@@ -233,6 +237,9 @@ def main():
 
     import vtkrylov as vk
     from vtkrylov import comm as vkcomm
+    # the GPU box runs the libvtkrylov.so pushed with the tree: refuse a binary that was not built
+    # from these sources (a stale build would be measured as this code)
+    build_id = vk._abi.check_build_id()
     ndev = vk.device_count()
     device = local % max(ndev, 1)
     ctx = vk.Context(device)
@@ -242,7 +249,7 @@ def main():
         else:
             vkcomm.init_host(ctx, rank, world)
     elif args.comm_solo:
-        os.environ["VTK_COMM_SOLO"] = "1"
+        ctx.set_tuning("comm_solo", 1)
         ctx.comm_init(0, 1, vk.Context.unique_id())
     ctx.set_orth(vk._abi.ORTH[args.orth])
     torch.cuda.set_device(device)
@@ -262,6 +269,23 @@ def main():
     offsets = vk.partition_rows(n_glob, world, align) if world > 1 else None
     t0 = time.time()
     A = vk.vlasov_operator(params, ctx=ctx, offsets=offsets)
+    if args.operator != "generated":
+        # the drop-in path: the operator arrives as a CSR (this rank's rows, global columns), the
+        # way the reference's scipy.sparse path would hand it; the library finds its structure
+        ip_h, ix_h, d_h = A.download()
+        A.close()
+        if args.operator == "npz":
+            import tempfile
+            from vtkrylov import npz as vknpz
+            tmpd = tempfile.mkdtemp(prefix="vtk_bench_")
+            f = os.path.join(tmpd, f"A_rank{rank}.npz")
+            vknpz.save_npz_arrays(f, ip_h, ix_h, d_h, (A.row_end - A.row_begin, n_glob), compressed=False)
+            del ip_h, ix_h, d_h
+            ip_h, ix_h, d_h, _ = vknpz.load_npz_arrays(f)
+            os.remove(f)
+            os.rmdir(tmpd)
+        A = vk.csr_matrix((d_h, ix_h, ip_h), shape=(n_glob, n_glob), ctx=ctx, offsets=offsets)
+        del ip_h, ix_h, d_h
     A.set_layout(args.layout)
     if args.prec == "line":
         M = vk.line_jacobi(A, vk.vlasov_line_stride(params), args.seg)
@@ -464,17 +488,21 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64" if not fp32 else "f32-values/f64",
-        "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), generated on device",
+        "data": "synthetic (SURVEY.md Appendix A Vlasov operator, splitmix64 RHS), " +
+                {"generated": "generated on device", "upload": "uploaded as a host CSR (vtkrylov.csr_matrix)",
+                 "npz": "read from a save_npz archive (vtkrylov.load_npz)"}[args.operator],
         "config": {"workload": f"{args.config}{'/' + str(args.slab) + ' slab' if args.slab > 1 else ''}: "
                                f"GMRES({args.restart}, {args.orth})+{mdesc} to rtol={args.rtol}, "
                                f"n={n_glob}, row-sharded over {world} GPU(s)",
                    "n": n_glob, "nnz": int(params_nnz(dim, shape)), "restart": args.restart,
-                   "prec": args.prec, "bs": args.bs if args.prec == "bj" else None,
+                   "prec": args.prec, "bs": args.bs if args.prec == "bj" else None, "operator": args.operator,
+                   "line_band": A.line_band, "line_values": A.line_values,
                    "seg": args.seg if args.prec == "line" else None, "bj_apply": mmode, "layout": A.layout, "rtol": args.rtol, "orth": args.orth,
                    "parallelism": f"row-slab x{world}",
                    "comm": args.comm if world > 1 else ("rccl-solo" if args.comm_solo else None),
                    "launcher": ("bench.py" if os.environ.get("VTK_BENCH_SPAWNED") else "external") if world > 1 else None},
         "rccl_ranks": ctx.rccl_ranks(),
+        "build_id": build_id,
         "inner_iters_per_solve": iters / args.steps,
         "solves_per_s": args.steps / elapsed,
         "solve_ms_median": sorted(per_solve)[len(per_solve) // 2] * 1e3,
@@ -524,7 +552,10 @@ def main():
         dist.destroy_process_group()
 
 
-KERNEL_SOURCES = ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp", "vtk_scalar.hpp")
+# every source whose text reaches device code: the kernels, the headers they include (geometry
+# constants and launch structs live in vtk_internal.hpp, the generator in vtk_vlasov.hpp)
+KERNEL_SOURCES = ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp", "vtk_scalar.hpp", "vtk_internal.hpp",
+                  "vtk_vlasov.hpp")
 
 
 def kernels_sha16():

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTK_ABI_VERSION 4
+#define VTK_ABI_VERSION 5
 
 typedef struct vtk_ctx vtk_ctx;
 typedef struct vtk_csr vtk_csr;
@@ -115,6 +115,11 @@ typedef struct {
 
 /* ---- library ------------------------------------------------------------------------ */
 int vtk_abi_version(void);
+/* 16 hex digits: SHA-256 of the library's sources (the .hip, .hpp and .cpp files of csrc, this
+ * header, the Makefile and its EXTRA flags) at build time.  Callers that ship a prebuilt binary next to the
+ * sources (the GPU box) compare it with the checked-out tree (vtkrylov._abi.check_build_id).
+ * (ABI 5) */
+const char *vtk_build_id(void);
 const char *vtk_status_string(int status);
 /* last error message of ctx (or of the last context-free call when ctx == NULL) */
 int vtk_last_error(vtk_ctx *ctx, char *buf, size_t len);
@@ -160,6 +165,15 @@ int vtk_ctx_create(int hip_device, vtk_ctx **out);      /* owns one hipStream_t 
 void vtk_ctx_destroy(vtk_ctx *ctx);
 int vtk_ctx_stream(vtk_ctx *ctx, void **hip_stream);    /* the stream all work runs on */
 int vtk_ctx_synchronize(vtk_ctx *ctx);
+/* Tuning switches of a context.  Defaults are the production path; the other
+ * settings exist for in-process A/B measurements and for the bit-identity tests (the same sums
+ * with and without a byte-saving form).  Each key is seeded from the environment variable
+ * VTK_<KEY in upper case> once, when the context is created; the library reads its environment
+ * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_canon_sl, sell_pad,
+ * sell_grid, plain_grid, lsv_spmv_cap, ev_every, prof_perj, debug_band, comm_solo, auto_band.
+ * VTK_ERR_ARG for an unknown key.  (ABI 5) */
+int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);
+int vtk_ctx_get_tuning(vtk_ctx *ctx, const char *key, int *value);
 /* rank 0 creates the 128-byte RCCL unique id; the caller broadcasts it (any transport) */
 int vtk_comm_unique_id(void *out128);
 int vtk_comm_init(vtk_ctx *ctx, int rank, int world, const void *rccl_unique_id);

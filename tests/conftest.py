@@ -51,6 +51,9 @@ def vk_lib():
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(PKG, "csrc")], check=True)
     import vtkrylov
     vtkrylov._abi.lib()
+    # the GPU box runs the prebuilt library pushed with the tree: it must be built from these
+    # sources (vtk_build_id), else every result below would describe other code
+    vtkrylov._abi.check_build_id()
     return vtkrylov
 
 

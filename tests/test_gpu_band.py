@@ -56,11 +56,12 @@ def test_band_not_set_on_4d_and_rejected_on_random(vk_lib, gpu):
 
 
 def test_band_explicit_on_uploaded_csr(vk_lib, gpu):
-    """A SciPy CSR of the 2D operator uploaded as plain CSR: set_line_band enables the path."""
+    """A SciPy CSR of the 2D operator uploaded as plain CSR with the detection off (line_len=0):
+    set_line_band enables the path (the default detection: tests/test_gpu_dropin.py)."""
     p = twin.CONFIGS["S2"]
     ip, ix, d = coracle.generate(p)
     import scipy.sparse as sp
-    A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu, line_len=0)
     assert A.line_band == 0
     A.set_line_band(p.shape[1])
     assert A.line_band == p.shape[1]
@@ -170,31 +171,22 @@ def test_band_line_separable_values_bit_identical(vk_lib, gpu, name):
     """The 2D Vlasov operators' values are line-separable (x couplings per position v, v couplings
     per line x; vtk_csr_get_line_values): the band step reads them from the tables -- the same
     values summed in the same order as from the SELL copy, so x is bit-identical with
-    VTK_BAND_LSV=0 (read per solve)."""
+    the context's band_lsv switch off."""
     import os
     p, A = _op(vk_lib, gpu, name)
     assert A.line_separable and A.line_values == 2   # the Vlasov rows are canonical too
     M = vk_lib.block_jacobi(A, 8)
     b = twin.rhs(p.n)
     x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
-    os.environ["VTK_BAND_LSV"] = "0"
-    try:
+    with gpu.tuning(band_lsv=0):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
-    finally:
-        del os.environ["VTK_BAND_LSV"]
     # canonical rows (the kinds' order from the row's line instead of the SELL codes) vs the codes
-    os.environ["VTK_BAND_CANON"] = "0"
-    try:
+    with gpu.tuning(band_canon=0):
         x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
-    finally:
-        del os.environ["VTK_BAND_CANON"]
     # the cycle-start SELL launches (residual + BJ, step 0's SpMV + BJ + dots) with their columns
     # from canon_row vs the codes
-    os.environ["VTK_SELL_CANON"] = "0"
-    try:
+    with gpu.tuning(sell_canon=0):
         x3, i3, s3 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
-    finally:
-        del os.environ["VTK_SELL_CANON"]
     assert s1.band == s0.band == s2.band == s3.band == 1 and i1 == i0 == i2 == i3 == 0
     assert s1.inner_iters == s0.inner_iters == s2.inner_iters == s3.inner_iters
     assert np.array_equal(x1, x0), "line-separable values change the band step's bits"
@@ -233,23 +225,17 @@ def test_band_not_separable_falls_back(vk_lib, gpu):
 def test_separable_values_in_unfused_paths_bit_identical(vk_lib, gpu, orth):
     """The solver's other SELL launches (fused SpMV + BJ + dots, residual, MGS matvec) also read
     the line-separable tables on such operators: with the band step off, x is bit-identical with
-    VTK_BAND_LSV=0 for both orthogonalisations."""
+    band_lsv off for both orthogonalisations."""
     import os
     p, A = _op(vk_lib, gpu, "C1")
     assert A.line_separable
     M = vk_lib.block_jacobi(A, 8)
     b = twin.rhs(p.n)
     x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
-    os.environ["VTK_BAND_LSV"] = "0"
-    try:
+    with gpu.tuning(band_lsv=0):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
-    finally:
-        del os.environ["VTK_BAND_LSV"]
-    os.environ["VTK_SELL_CANON"] = "0"   # the SELL codes instead of canon_row's columns
-    try:
+    with gpu.tuning(sell_canon=0):   # the SELL codes instead of canon_row's columns
         x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
-    finally:
-        del os.environ["VTK_SELL_CANON"]
     assert s1.band == s0.band == s2.band == 0 and i1 == i0 == i2 == 0
     assert s1.inner_iters == s0.inner_iters == s2.inner_iters
     assert np.array_equal(x1, x0)

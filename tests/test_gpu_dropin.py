@@ -1,0 +1,136 @@
+"""The drop-in path gets the fast solver: a CSR handed over the way the
+reference's scipy.sparse path would hand it -- ``vtkrylov.csr_matrix`` of a SciPy matrix, of
+host arrays or of device tensors, ``vtkrylov.load_npz`` of a ``save_npz`` archive -- is checked
+for the 2D Vlasov x-line structure inside ``vtk_csr_create`` (candidate line length from the
+first and last rows' columns, then the same device checks as ``vtk_csr_set_line_band``).  When
+it holds, the operator gets the line band, the line-separable tables and canonical rows, and
+GMRES runs the band step exactly as on the generated operator: the same bits.
+"""
+import numpy as np
+import pytest
+
+from oracle import coracle, twin
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(vk, A, M, b, **kw):
+    x, info = vk.gmres(A, b, rtol=kw.pop("rtol", 1e-8), M=M, **kw)
+    return x, info, vk.last_stats()
+
+
+@pytest.mark.parametrize("name", ["S2", "C1"])
+@pytest.mark.parametrize("how", ["scipy", "arrays", "device", "npz"])
+def test_uploaded_csr_runs_the_band_step_bit_identical(vk_lib, gpu, tmp_path, name, how):
+    import scipy.sparse as sp
+    p = twin.CONFIGS[name]
+    G = vk_lib.vlasov_operator(vk_lib.vlasov_params(p.dim, p.shape), ctx=gpu)
+    ip, ix, d = G.download()
+    if how == "scipy":
+        A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    elif how == "arrays":
+        A = vk_lib.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=gpu)
+    elif how == "device":
+        import torch
+        dev = torch.device("cuda", gpu.device)
+        A = vk_lib.csr_matrix((torch.from_numpy(d).to(dev), torch.from_numpy(ix).to(dev),
+                               torch.from_numpy(ip).to(dev)), shape=(p.n, p.n), ctx=gpu)
+    else:
+        f = tmp_path / "A.npz"
+        sp.save_npz(f, sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)))
+        A = vk_lib.load_npz(f, ctx=gpu)
+    assert A.line_band == G.line_band == p.shape[1]
+    assert A.line_values == G.line_values == 2     # separable values, canonical rows
+    b = twin.rhs(p.n)
+    MG, MA = vk_lib.block_jacobi(G, 8), vk_lib.block_jacobi(A, 8)
+    xg, ig, sg = _solve(vk_lib, G, MG, b)
+    xa, ia, sa = _solve(vk_lib, A, MA, b)
+    assert sg.band == sa.band == 1 and ig == ia == 0
+    assert sa.inner_iters == sg.inner_iters
+    assert np.array_equal(xa, xg), "uploaded operator's solve differs from the generated one's"
+    for o in (MG, MA, A, G):
+        o.close()
+
+
+def test_line_len_argument(vk_lib, gpu):
+    """line_len=0 keeps the plain path; an explicit line length is required to hold."""
+    import scipy.sparse as sp
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = coracle.generate(p)
+    S = sp.csr_matrix((d, ix, ip), shape=(p.n, p.n))
+    A0 = vk_lib.csr_matrix(S, ctx=gpu, line_len=0)
+    assert A0.line_band == 0 and A0.line_values == 0
+    M0 = vk_lib.block_jacobi(A0, 8)
+    x0, i0, s0 = _solve(vk_lib, A0, M0, coracle.rhs(p.n))
+    assert s0.band == 0 and i0 == 0
+    A1 = vk_lib.csr_matrix(S, ctx=gpu, line_len=p.shape[1])
+    assert A1.line_band == p.shape[1]
+    with pytest.raises(ValueError):
+        vk_lib.csr_matrix(S, ctx=gpu, line_len=2 * p.shape[1])   # no such structure
+    for o in (M0, A0, A1):
+        o.close()
+
+
+def test_detection_can_be_switched_off(vk_lib, gpu):
+    import scipy.sparse as sp
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = coracle.generate(p)
+    with gpu.tuning(auto_band=0):
+        A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    assert A.line_band == 0
+    A.close()
+
+
+@pytest.mark.parametrize("name", ["C0", "S4"])
+def test_no_band_where_there_is_none(vk_lib, gpu, name):
+    """1D (every coupling within one row) and 4D (x couplings Ny*Nvx*Nvy rows away): the
+    candidate fails the device check, the operator keeps the plain path, nothing raises."""
+    p = twin.CONFIGS[name]
+    ip, ix, d = coracle.generate(p)
+    A = vk_lib.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=gpu)
+    assert A.line_band == 0
+    M = vk_lib.block_jacobi(A, 8)
+    b = coracle.rhs(p.n)
+    x, info, st = _solve(vk_lib, A, M, b)
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    assert st.band == 0 and info == ref.info == 0
+    assert abs(st.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    M.close()
+    A.close()
+
+
+def test_ragged_and_random_csr_unaffected(vk_lib, gpu):
+    """Ragged random CSR (empty rows, a long row): no line band, SpMV still bit-identical to SciPy."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(7)
+    n = 2000
+    R = sp.random(n, n, density=0.003, random_state=11, format="csr") + sp.identity(n, format="csr")
+    R = R.tolil()
+    R[5, :] = 0
+    R[17, rng.choice(n, 600, replace=False)] = 1.5
+    R = R.tocsr()
+    A = vk_lib.csr_matrix(R, ctx=gpu)
+    assert A.line_band == 0
+    x = rng.standard_normal(n)
+    assert np.array_equal(A @ x, R @ x)
+    A.close()
+
+
+def test_device_csr_overlong_indptr_rejected(vk_lib, gpu):
+    """indptr[-1] beyond the index / value tensors is refused before any copy."""
+    import torch
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = coracle.generate(p)
+    dev = torch.device("cuda", gpu.device)
+    ipt = torch.from_numpy(ip.copy()).to(dev)
+    ipt[-1] = ix.shape[0] + 1000
+    with pytest.raises(ValueError):
+        vk_lib.csr_matrix((torch.from_numpy(d).to(dev), torch.from_numpy(ix).to(dev), ipt), shape=(p.n, p.n), ctx=gpu)
+    with pytest.raises(ValueError):   # wrong indptr length
+        vk_lib.csr_matrix((torch.from_numpy(d).to(dev), torch.from_numpy(ix).to(dev),
+                           torch.from_numpy(ip[:-1].copy()).to(dev)), shape=(p.n, p.n), ctx=gpu)
+    with pytest.raises(ValueError):   # host arrays, too
+        ip2 = ip.copy()
+        ip2[-1] += 5
+        vk_lib.csr_matrix((d, ix, ip2), shape=(p.n, p.n), ctx=gpu)

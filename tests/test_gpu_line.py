@@ -300,7 +300,7 @@ def test_gmres_line_full_size(gpu, vk_lib, name):
 def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
     """On a line-separable operator the line path's SpMV reads the values from the tables
     (k_lsv_spmv): k_sell's plain sum in the same order, so the solve is
-    bit-identical with VTK_BAND_LSV=0 (the SELL values; read per solve)."""
+    bit-identical with band_lsv off (the SELL values)."""
     import os
     import numpy as np
     from oracle import twin
@@ -311,18 +311,12 @@ def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
     b = twin.rhs(p.n)
     x1, i1 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
     it1 = vk_lib.last_stats().inner_iters
-    os.environ["VTK_BAND_LSV"] = "0"
-    try:
+    with gpu.tuning(band_lsv=0):
         x0, i0 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
-    finally:
-        del os.environ["VTK_BAND_LSV"]
     assert i1 == i0 == 0 and it1 == vk_lib.last_stats().inner_iters
     assert np.array_equal(x1, x0)
-    os.environ["VTK_SELL_CANON"] = "0"   # the SELL codes instead of canon_row's columns
-    try:
+    with gpu.tuning(sell_canon=0):   # the SELL codes instead of canon_row's columns
         x2, i2 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
-    finally:
-        del os.environ["VTK_SELL_CANON"]
     assert i2 == 0 and it1 == vk_lib.last_stats().inner_iters
     assert np.array_equal(x1, x2)
     M.close()

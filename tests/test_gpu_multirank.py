@@ -43,8 +43,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
         A = vk.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=ctx, offsets=offs)
     else:           # device assembly of this rank's rows
         A = vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=ctx, offsets=offs)
-    if from_host and p.dim == 2:   # declared by hand on an uploaded CSR (auto on vlasov_operator)
-        A.set_line_band(p.shape[1])
+    # the line band is found in the CSR on every path (device assembly, host row blocks, npz)
+    assert A.line_band == (p.shape[1] if p.dim == 2 else 0), A.line_band
     x = twin.rhs(p.n, seed=0xC0FFEE)
     y = A @ x[rb:re_]
     M = vk.block_jacobi(A, 8)

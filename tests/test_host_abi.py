@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(vk_lib):
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(vk_lib._abi.PROTOTYPES), set(names) ^ set(vk_lib._abi.PROTOTYPES)
-    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 4
+    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 5
 
 
 def test_status_strings(vk_lib):
@@ -149,6 +149,46 @@ def test_library_is_current():
         [os.path.join(root, "include", "vtkrylov.h")]
     stale = [s for s in srcs if os.path.getmtime(s) > os.path.getmtime(so)]
     assert not stale, f"libvtkrylov.so is older than {stale}"
+
+
+def test_build_id_matches_sources(vk_lib):
+    """vtk_build_id() is the SHA-256 of the sources the library was built from (csrc/Makefile);
+    _abi.source_build_id() recomputes it over the checked-out tree: equal for a current build."""
+    bid = vk_lib._abi.build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid)
+    assert bid == vk_lib._abi.source_build_id()
+    assert vk_lib._abi.check_build_id() == bid
+
+
+def test_build_id_mismatch_is_refused(vk_lib, tmp_path, monkeypatch):
+    """A library built from other sources (the GPU box runs the binary pushed with the tree) is
+    refused: one changed byte in any source changes the id, and check_build_id raises."""
+    import shutil
+    src = os.path.join(os.path.dirname(vk_lib._abi.CSRC), "csrc")
+    d = tmp_path / "csrc"
+    shutil.copytree(src, d, ignore=shutil.ignore_patterns("build"))
+    hdr = tmp_path / "vtkrylov.h"
+    shutil.copy(vk_lib._abi.HEADER, hdr)
+    same = vk_lib._abi.source_build_id(str(d), str(hdr))
+    assert same == vk_lib._abi.build_id()
+    with open(d / "vtk_band.hip", "ab") as f:
+        f.write(b"\n// edited\n")
+    other = vk_lib._abi.source_build_id(str(d), str(hdr))
+    assert other != same
+    monkeypatch.delenv("VTK_LIB", raising=False)
+    with pytest.raises(vk_lib._abi.StaleBuildError):
+        vk_lib._abi.check_build_id(sources=other)
+    # EXTRA build flags are part of the id too
+    assert vk_lib._abi.source_build_id(str(d), str(hdr), extra="-DX=1") != other
+
+
+def test_tuning_keys_without_gpu(vk_lib):
+    """vtk_ctx_set_tuning / get_tuning need a context (no GPU here): NULL context -> VTK_ERR_ARG."""
+    import ctypes
+    L = vk_lib._abi.lib()
+    v = ctypes.c_int()
+    assert L.vtk_ctx_set_tuning(None, b"band", 0) == vk_lib._abi.ERR_ARG
+    assert L.vtk_ctx_get_tuning(None, b"band", ctypes.byref(v)) == vk_lib._abi.ERR_ARG
 
 
 @pytest.mark.slow

@@ -2,11 +2,11 @@
 settings): the band step's rate varies ~5 % between processes with the physical placement of
 the same allocations (profiles/r03_membench_walk.txt), so A/Bs across processes need many reps.
 
-    python tools/ab_env.py --env VTK_BAND --values 1,0 --rounds 6 [--config C3] [--slab 8 --comm-solo]
+    python tools/ab_env.py --env band --values 1,0 --rounds 6 [--config C3] [--slab 8 --comm-solo]
 
-Prints one JSON line: per value the solve wall times (ms) and their median.  The switch must be
-one the library reads per solve (VTK_BAND; VTK_BAND_CHAIN of the dropped band-tail experiment,
-profiles/r03_chain_ab.json)."""
+Prints one JSON line: per value the solve wall times (ms) and their median.  The switch is a
+context tuning key (vtk_ctx_set_tuning: band, band_lsv, sell_canon, ...; a VTK_<KEY> name is
+accepted too), set on the context between solves."""
 import argparse
 import json
 import os
@@ -37,7 +37,7 @@ def main():
     p = twin.CONFIGS[a.config]
     ctx = vk.default_context(0)
     if a.comm_solo:
-        os.environ["VTK_COMM_SOLO"] = "1"
+        ctx.set_tuning("comm_solo", 1)
         ctx.comm_init(0, 1, vk.Context.unique_id())
     shape = (p.shape[0] // a.slab,) + tuple(p.shape[1:])
     n = int(np.prod(shape))
@@ -47,12 +47,13 @@ def main():
     import torch
     b = torch.from_numpy(vk.rhs_splitmix(n)).to(torch.device("cuda", 0))   # device-resident, as bench.py
     torch.cuda.synchronize()
+    key = a.env[4:].lower() if a.env.startswith("VTK_") else a.env
     vals = a.values.split(",")
     times = {v: [] for v in vals}
     iters = {}
     for r in range(a.rounds + 1):
         for v in (vals if r % 2 == 0 else vals[::-1]):
-            os.environ[a.env] = v
+            ctx.set_tuning(key, int(v))
             t = time.perf_counter()
             _, info = vk.gmres(A, b, rtol=a.rtol, M=M)
             dt = (time.perf_counter() - t) * 1e3

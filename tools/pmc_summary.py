@@ -22,6 +22,7 @@ import csv
 import hashlib
 import json
 import os
+import sys
 import re
 import shutil
 import statistics
@@ -111,11 +112,9 @@ def main():
     durations = trace_durations(os.path.join(src, a.prof, "run_kernel_trace.csv"))
     fetch = load(os.path.join(src, a.fetch, "run_counter_collection.csv"))
     write = load(os.path.join(src, a.write, "run_counter_collection.csv"))
-    hsh = hashlib.sha256()   # the device sources, in bench.py's KERNEL_SOURCES order
-    for name in ("vtk_kernels.hip", "vtk_band.hip", "vtk_device.hpp", "vtk_scalar.hpp"):
-        with open(os.path.join(root, "vt-precondition_amd", "csrc", name), "rb") as f:
-            hsh.update(f.read())
-    ksha = hsh.hexdigest()[:16]
+    sys.path.insert(0, root)
+    import bench   # the device sources, hashed in bench.py's KERNEL_SOURCES order
+    ksha = bench.kernels_sha16()
     out = {"_how": ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                     f"'{a.cmd}'; "
                     "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "

@@ -9,6 +9,7 @@
 // after the stop column return at entry (GmresState::stop_col), so the host enqueues a cycle
 // without a per-step round trip and throttles itself with events LOOKAHEAD columns behind.
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -72,6 +73,31 @@ int dalloc(vtk_ctx *c, DBuf &b, size_t bytes) {
 }
 
 int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+// ---- tuning switches (vtk::Tuning): name, member; VTK_<NAME upper> seeds them at creation ----
+struct TuneKey { const char *name; int Tuning::*mem; };
+constexpr TuneKey TUNE_KEYS[] = {
+    {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
+    {"band_canon", &Tuning::band_canon}, {"band_canon_sl", &Tuning::band_canon_sl},
+    {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid},
+    {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
+    {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
+};
+
+const TuneKey *tune_key(const char *name) {
+    if (!name) return nullptr;
+    for (const auto &k : TUNE_KEYS)
+        if (std::strcmp(k.name, name) == 0) return &k;
+    return nullptr;
+}
+
+void tune_from_env(Tuning &t) {
+    for (const auto &k : TUNE_KEYS) {
+        std::string var = "VTK_";
+        for (const char *p = k.name; *p; ++p) var += (char)std::toupper((unsigned char)*p);
+        if (const char *e = std::getenv(var.c_str()); e && *e) t.*k.mem = std::atoi(e);
+    }
+}
 
 // ---- kernel profile: HIP events around each launch on the context stream ------------------
 hipEvent_t prof_event(vtk_ctx *c) {
@@ -313,6 +339,7 @@ SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nu
         in.sell = &A->sell;
         in.groups = g ? g : &A->g_all;
     }
+    in.plain_grid = A->ctx->tune.plain_grid;
     return in;
 }
 
@@ -325,11 +352,10 @@ bool bj_fused(const vtk_prec *M) {
 }
 
 // the solver's SELL launches read the line-separable tables when the operator
-// has them: the same values, the same sums, 8 B of values per row instead of 40 (VTK_BAND_LSV=0:
-// the SELL values; read per call).  vtk_spmv keeps the SELL values: it is the measured SpMV
+// has them: the same values, the same sums, 8 B of values per row instead of 40 (tuning band_lsv
+// 0: the SELL values).  vtk_spmv keeps the SELL values: it is the measured SpMV
 bool lsv_on(const vtk_csr *A) {
-    const char *e = std::getenv("VTK_BAND_LSV"), *e2 = std::getenv("VTK_SELL_LSV");
-    return A->use_sell && A->d_lsv && A->band_L > 0 && !A->fp32 && !(e && e[0] == '0') && !(e2 && e2[0] == '0') &&
+    return A->use_sell && A->d_lsv && A->band_L > 0 && !A->fp32 && A->ctx->tune.band_lsv &&
            (!A->ctx->dist || A->band_ghost);
 }
 SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
@@ -337,9 +363,8 @@ SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
         in.lsv = A->d_lsv;
         in.lsv_L = (int)A->band_L;
         in.lsv_lblk = A->band_ghost ? A->band_lblk : -1;
-        // VTK_SELL_CANON=0 (A/B, read per launch): the SELL codes even for canonical rows
-        const char *e = std::getenv("VTK_SELL_CANON");
-        in.lsv_canon = A->lsv_canon && !(e && e[0] == '0') ? 1 : 0;
+        // tuning sell_canon 0 (A/B): the SELL codes even for canonical rows
+        in.lsv_canon = A->lsv_canon && A->ctx->tune.sell_canon ? 1 : 0;
     }
     return in;
 }
@@ -348,8 +373,7 @@ double matrix_bytes(const vtk_csr *A);
 double solver_matrix_bytes(const vtk_csr *A) {
     const double b = matrix_bytes(A);
     if (!lsv_on(A)) return b;
-    const char *e = std::getenv("VTK_SELL_CANON");
-    if (A->lsv_canon && !(e && e[0] == '0')) return 8.0 * (double)A->n_local;   // the diagonal only
+    if (A->lsv_canon && A->ctx->tune.sell_canon) return 8.0 * (double)A->n_local;   // the diagonal only
     return b - 8.0 * (double)A->sell.entries + 8.0 * (double)A->n_local;
 }
 
@@ -483,7 +507,7 @@ int build_sell(vtk_csr *A, bool only_if_compact, bool *built) {
     // entry narrower) are padded to the widest chunk when that costs <= 2 % more entries: every
     // chunk's offset is then 64 W q and the kernels take the compile-time-width path (no offset
     // loads at the head of each chunk)
-    if (nch > 0 && std::getenv("VTK_SELL_NOPAD") == nullptr) {
+    if (nch > 0 && c->tune.sell_pad) {
         std::vector<int64_t> off((size_t)nch + 1);
         e = hipMemcpy(off.data(), sl.d_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost);
         if (e != hipSuccess) { drop(); return fail(c, VTK_ERR_HIP, std::string("SELL build: ") + hipGetErrorString(e)); }
@@ -574,8 +598,8 @@ int build_groups(vtk_csr *A) {
     const int ng = (int)((A->n_local + 255) / 256);
     A->g_all.count = ng;
     A->g_all.grid = grid_for(c, std::max(1, std::min(ng, GMAX)));
-    if (const char *e = std::getenv("VTK_SELL_GRID"); e && !c->dist)   // tuning experiments
-        A->g_all.grid = std::max(1, std::min({ng, GMAX, std::atoi(e)}));
+    if (c->tune.sell_grid > 0 && !c->dist)   // tuning experiments
+        A->g_all.grid = std::max(1, std::min({ng, GMAX, c->tune.sell_grid}));
     if (c->dist && A->row_halo.size() == (size_t)A->n_local) {
         std::vector<int32_t> gi, gb;
         for (int g = 0; g < ng; ++g) {
@@ -720,9 +744,11 @@ struct BandCheck {
 int band_check(vtk_csr *A, int64_t L, BandCheck &out) {
     vtk_ctx *c = A->ctx;
     const int64_t n = A->n_local;
-    // whole lines, >= 2 of them, rows and halo columns within the kernels' 32-bit indices
-    vtk_band_geometry geo{};
-    if (vtk_line_band_plan(n, L, c->n_cu, &geo) != VTK_OK) return VTK_ERR_ARG;
+    // the structure only: whole lines, >= 2 of them, rows and the two halo lines within the
+    // kernels' 32-bit indices.  Whether the band STEP can run on it (line parts of <= 400 rows,
+    // multiples of 8: vtk_line_band_plan) is run_gmres's decision; the line path's table SpMV and
+    // the SELL launches need the structure alone.
+    if (L <= 0 || n <= 0 || n % L != 0 || n / L < 2 || n + 2 * L >= INT32_MAX / 2) return VTK_ERR_ARG;
     bool solo = true;
     if (c->dist && band_check_dist(A, L, solo, out.lay) != VTK_OK) return VTK_ERR_ARG;
     if (solo && n / L < 3) return VTK_ERR_ARG;
@@ -747,12 +773,37 @@ int band_check_all(vtk_csr *A, int64_t L) {
     vtk_ctx *c = A->ctx;
     BandCheck chk;
     int rc = band_check(A, L, chk);
-    static const bool dbg = [] { const char *e = std::getenv("VTK_DEBUG_BAND"); return e && e[0] == '1'; }();
-    if (dbg)
+    if (c->tune.debug_band)
         std::fprintf(stderr, "[vtk band] rank %d/%d L=%lld n_local=%lld n_halo=%lld n_send=%lld local rc=%d vloc=%d ghost=%d\n",
                      c->rank, c->world, (long long)L, (long long)A->n_local, (long long)A->n_halo, (long long)A->n_send, rc,
                      (int)chk.vloc, (int)chk.ghost);
+    // line-separable values (rank-local: the kernels read them or the SELL values, the same bits
+    // either way): built into a scope-owned buffer and checked against the CSR bit for bit;
+    // committed below together with the layout only once every rank has passed
+    DBuf lsv;
+    bool lsv_ok = false, canon = false;
+    const int64_t n = A->n_local;
+    if (rc == VTK_OK && !A->fp32) {
+        const size_t nl = (size_t)n + 2 * (size_t)L + 2 * (size_t)(n / L);
+        DBuf bad;
+        rc = dalloc(c, lsv, nl * sizeof(double));
+        if (rc == VTK_OK) rc = dalloc(c, bad, sizeof(int));
+        int hb = 1;
+        hipError_t e = hipSuccess;
+        if (rc == VTK_OK) e = hipMemsetAsync(lsv.p, 0, nl * sizeof(double), c->stream);
+        if (rc == VTK_OK && e == hipSuccess) e = hipMemsetAsync(bad.p, 0, sizeof(int), c->stream);
+        if (rc == VTK_OK && e == hipSuccess)
+            e = launch_lsv_build(A->d_indptr, A->d_indices, static_cast<const double *>(A->d_data), n, (int)L,
+                                 chk.ghost ? chk.lay.lblk : -1, lsv.as<double>(), bad.as<int>(), c->stream);
+        if (rc == VTK_OK && e == hipSuccess) e = hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+        if (rc == VTK_OK && e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (rc == VTK_OK && e != hipSuccess)
+            rc = fail(c, e == hipErrorOutOfMemory ? VTK_ERR_NOMEM : VTK_ERR_HIP, std::string("line values: ") + hipGetErrorString(e));
+        lsv_ok = rc == VTK_OK && (hb & 1) == 0;
+        canon = lsv_ok && (hb & 2) == 0;
+    }
     if (c->dist) {
+        // the agreement runs even after a local failure: every rank joins the same collective
         double mine = rc == VTK_OK ? 0.0 : 1.0, bad = 0.0;
         HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
         TRY(comm_allreduce(c, &c->d_scal[DC_NQ], 1));
@@ -761,7 +812,7 @@ int band_check_all(vtk_csr *A, int64_t L) {
         if (rc == VTK_OK && bad != 0.0) rc = VTK_ERR_ARG;
     }
     if (rc != VTK_OK) return rc;
-    // every rank passed: commit the layout together with band_L (set by the caller)
+    // every rank passed: commit the layout and the tables (band_L is set by the caller)
     A->band_vloc = chk.vloc;
     A->band_ghost = chk.ghost;
     A->band_lblk = chk.lay.lblk;
@@ -775,33 +826,71 @@ int band_check_all(vtk_csr *A, int64_t L) {
     A->band_off_last = chk.lay.off_last;
     A->band_off_left = chk.lay.off_left;
     A->band_off_right = chk.lay.off_right;
-    // line-separable values (rank-local: the band step reads them or the SELL values, the same
-    // bits either way): built and checked against the CSR bit for bit, dropped when they do not
-    // reproduce it (f64 values only)
     (void)hipFree(A->d_lsv);
     A->d_lsv = nullptr;
     A->lsv_canon = false;
-    const int64_t n = A->n_local;
-    if (!A->fp32 && n % L == 0) {
-        const size_t nl = (size_t)n + 2 * (size_t)L + 2 * (size_t)(n / L);
-        double *lsv = nullptr;
-        HIPCHK(c, hipMalloc(&lsv, nl * sizeof(double)));
-        DBuf bad;
-        TRY(dalloc(c, bad, sizeof(int)));
-        HIPCHK(c, hipMemsetAsync(lsv, 0, nl * sizeof(double), c->stream));
-        HIPCHK(c, hipMemsetAsync(bad.p, 0, sizeof(int), c->stream));
-        HIPCHK(c, launch_lsv_build(A->d_indptr, A->d_indices, static_cast<const double *>(A->d_data), n, (int)L,
-                                   chk.ghost ? chk.lay.lblk : -1, lsv, bad.as<int>(), c->stream));
-        int hb = 1;
-        HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if ((hb & 1) == 0) {
-            A->d_lsv = lsv;
-            A->lsv_canon = (hb & 2) == 0;
-        } else {
-            (void)hipFree(lsv);
-        }
+    if (lsv_ok) {
+        A->d_lsv = lsv.as<double>();
+        lsv.p = nullptr;   // owned by the operator now
+        A->lsv_canon = canon;
     }
+    return VTK_OK;
+}
+
+// Line length the drop-in path (vtk_csr_create) tries: the smallest column distance > 1
+// (periodic in n) that the first and the last local row both couple to -- for the 2D Vlasov
+// operators Nv, their x-neighbour couplings (row = x Nv + v).  0 when there is none.  Collective
+// (world > 1): the ranks' candidates must agree, else 0 everywhere.
+int line_len_candidate(vtk_csr *A, int64_t &L) {
+    vtk_ctx *c = A->ctx;
+    const int64_t n = A->n_local, N = A->n_global;
+    L = 0;
+    std::vector<int64_t> d[2];
+    if (n >= 1) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (int s = 0; s < 2; ++s) {
+            const int64_t r = s == 0 ? 0 : n - 1;
+            const int32_t k0 = A->h_indptr[(size_t)r], k1 = A->h_indptr[(size_t)r + 1];
+            std::vector<int32_t> idx((size_t)std::max(0, k1 - k0));
+            if (k1 > k0) HIPCHK(c, hipMemcpy(idx.data(), A->d_indices + k0, (k1 - k0) * sizeof(int32_t), hipMemcpyDeviceToHost));
+            for (int32_t l : idx) {
+                const int64_t g = l < n ? l + A->row_begin : A->halo_cols[(size_t)(l - n)];
+                int64_t dist = std::llabs(g - (A->row_begin + r));
+                dist = std::min(dist, N - dist);
+                if (dist > 1) d[s].push_back(dist);
+            }
+            std::sort(d[s].begin(), d[s].end());
+        }
+        for (int64_t v : d[0])
+            if (std::binary_search(d[1].begin(), d[1].end(), v)) { L = v; break; }
+    }
+    if (c->dist) {
+        const int W = c->world;
+        DBuf mine, all;
+        TRY(dalloc(c, mine, sizeof(int64_t)));
+        TRY(dalloc(c, all, (size_t)W * sizeof(int64_t)));
+        HIPCHK(c, hipMemcpyAsync(mine.p, &L, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+        TRY(comm_allgather_i64(c, mine.as<int64_t>(), all.as<int64_t>(), 1));
+        std::vector<int64_t> h((size_t)W);
+        HIPCHK(c, hipMemcpyAsync(h.data(), all.p, W * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (int64_t v : h)
+            if (v != h[0]) { L = 0; break; }
+        if (L != 0) L = h[0];
+    }
+    return VTK_OK;
+}
+
+// the drop-in path's line-band detection: the same check vtk_csr_set_line_band runs, on the
+// candidate line length (tuning auto_band 0: off)
+int auto_line_band(vtk_csr *A) {
+    if (!A->ctx->tune.auto_band) return VTK_OK;
+    int64_t L = 0;
+    TRY(line_len_candidate(A, L));
+    if (L <= 0) return VTK_OK;   // uniform across ranks: nobody enters the collective below
+    const int rc = band_check_all(A, L);
+    if (rc == VTK_OK) A->band_L = L;
+    else if (rc != VTK_ERR_ARG) return rc;
     return VTK_OK;
 }
 
@@ -892,16 +981,14 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
                          s.M->line.seg <= 32 && s.G <= GMAX;
     // line path on a line-separable operator: the SpMV from the tables (VTK_BAND_LSV=0: SELL)
-    const char *lsv_e0 = std::getenv("VTK_BAND_LSV");
-    const bool line_lsv = line_dc && s.A->d_lsv && s.A->band_L > 0 && !(lsv_e0 && lsv_e0[0] == '0') && s.A->use_sell &&
+    const bool line_lsv = line_dc && s.A->d_lsv && s.A->band_L > 0 && c->tune.band_lsv && s.A->use_sell &&
                           s.A->sell.uniform_w == 5 && s.A->sell.d_pk && s.A->sell.n_wide == 0 &&
                           (!c->dist || s.A->band_ghost);
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = matrix_bytes(s.A);
     const double b_lsv = b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n;
-    // canonical rows: the diagonal only (VTK_SELL_CANON=0: the codes too; A/B)
-    const char *canon_l = std::getenv("VTK_SELL_CANON");
-    const bool line_canon = line_lsv && s.A->lsv_canon && !(canon_l && canon_l[0] == '0');
+    // canonical rows: the diagonal only (tuning sell_canon 0: the codes too; A/B)
+    const bool line_canon = line_lsv && s.A->lsv_canon && c->tune.sell_canon;
     const double b_inv = bj_row_bytes(s.M) * n;
     // dots (unless the SpMV wrote them: cnt partials), all-reduce across ranks, scalar step
     // (folding the finalize into the boundary launch's last workgroup was measured slower: one
@@ -932,24 +1019,18 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         return VTK_OK;
     };
     const bool band = s.band;
-    // line-separable values in the band step (VTK_BAND_LSV=0: the SELL values; read per solve)
-    const char *lsv_e = std::getenv("VTK_BAND_LSV");
-    const bool band_lsv = band && s.A->d_lsv && !(lsv_e && lsv_e[0] == '0');
-    const char *canon_e = std::getenv("VTK_BAND_CANON");   // 0: read the codes anyway (A/B)
-    const char *canon_sl_e = std::getenv("VTK_BAND_CANON_SL");   // 0: the per-entry loop (A/B)
-    const bool canon_sl = !(canon_sl_e && canon_sl_e[0] == '0');
+    // line-separable values in the band step (tuning band_lsv 0: the SELL values)
+    const bool band_lsv = band && s.A->d_lsv && c->tune.band_lsv;
+    const bool band_canon = c->tune.band_canon != 0;       // 0: read the codes anyway (A/B)
+    const bool canon_sl = c->tune.band_canon_sl != 0;      // 0: the per-entry loop (A/B)
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)
-    const double b_band = band_lsv ? (s.A->lsv_canon && !(canon_e && canon_e[0] == '0')
+    const double b_band = band_lsv ? (s.A->lsv_canon && band_canon
                                           ? 8.0 * (double)n   // the diagonal only
                                           : b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n)
                                    : b_csr;
     bool broke = false;
-    static const int ev_every = [] {
-        const char *e = std::getenv("VTK_EV_EVERY");
-        const int v = e ? std::atoi(e) : 1;
-        return v >= 1 && v <= LOOKAHEAD + 1 ? v : 1;
-    }();
+    const int ev_every = c->tune.ev_every >= 1 && c->tune.ev_every <= LOOKAHEAD + 1 ? c->tune.ev_every : 1;
     int ev_step[LOOKAHEAD + 1];
     int nev = 0, synced = 0;
     for (int j = 0; j < m; ++j) {
@@ -1001,7 +1082,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
                                           s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
-                                          c->stream, line_canon ? 1 : 0));
+                                          c->stream, line_canon ? 1 : 0, c->tune.lsv_spmv_cap));
             } else {
                 Prof pf(c, "spmv", j, b_csr + 2 * n8);
                 HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
@@ -1038,7 +1119,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             // reads V_k (k < j), w_{j-1} (v_0 at j = 0), w_j; writes v_j (j >= 1), w_{j+1} and, at
             // j = m - 2 only, p_{j+1} (k_dc_update's operand)
             // (VTK_PROF_PERJ=1: one profile class per step index, "band_step_jNN")
-            static const bool perj = [] { const char *e = std::getenv("VTK_PROF_PERJ"); return e && e[0] == '1'; }();
+            const bool perj = c->tune.prof_perj != 0;
             static const char *const jname[] = {"band_step_j00", "band_step_j01", "band_step_j02", "band_step_j03",
                 "band_step_j04", "band_step_j05", "band_step_j06", "band_step_j07", "band_step_j08", "band_step_j09",
                 "band_step_j10", "band_step_j11", "band_step_j12", "band_step_j13", "band_step_j14", "band_step_j15",
@@ -1069,7 +1150,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
-            a.canon = band_lsv && s.A->lsv_canon && !(canon_e && canon_e[0] == '0') ? (canon_sl ? 2 : 1) : 0;
+            a.canon = band_lsv && s.A->lsv_canon && band_canon ? (canon_sl ? 2 : 1) : 0;
             HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
@@ -1117,10 +1198,8 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const size_t ndc = dc ? (size_t)(m + 1) * (m + 1) + sizeof(DcCoef) / 8 + 8 + (size_t)DC_NQ * GMAX : 0;
     // line-band DCGS2 step: one rank, SELL of uniform width 5 with coded columns (no wide chunk),
     // f64 values, tridiagonal BJ(8) (the fused step's TRIM apply), restart <= 20
-    // VTK_BAND=0: the band step off (read per solve: tools/ab_env.py alternates it in one process)
-    const char *band_e = std::getenv("VTK_BAND");
-    const bool band_env = !(band_e && band_e[0] == '0');
-    s.band = dc && band_env && c->band && A->band_L > 0 && A->band_L % 8 == 0 &&
+    // tuning band 0 (vtk_gmres_set_band): the band step off (tools/ab_env.py alternates it)
+    s.band = dc && c->tune.band && A->band_L > 0 && A->band_L % 8 == 0 &&
              (!c->dist || !A->band_ghost || c->comm || c->host_comm) &&
              A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && !A->fp32 && M &&
              M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_fused(M) && bj_op(M).tri != nullptr && m >= 2 && m <= 20;
@@ -1138,8 +1217,14 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         }
     }
     // every rank takes the same path: the band step exchanges ghost lines with its neighbours
-    // each step, so one rank falling back alone would leave its peers' sends unmatched
-    if (c->dist) {
+    // each step, so one rank falling back alone would leave its peers' sends unmatched.  The
+    // agreement (an all-reduce and a host sync) is needed only when some rank could take the band:
+    // the inputs below are the same on every rank (band_L is set on all ranks or none; the
+    // orthogonalisation, the switch, the preconditioner and restart are the callers' uniform
+    // arguments), the rest (layout, geometry) is rank-local
+    const bool band_possible = dc && c->tune.band && A->band_L > 0 && M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 &&
+                               m >= 2 && m <= 20;
+    if (c->dist && band_possible) {
         double mine = s.band ? 0.0 : 1.0;
         HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
         TRY(comm_allreduce(c, &c->d_scal[DC_NQ], 1));
@@ -1405,6 +1490,7 @@ int vtk_ctx_create(int device, vtk_ctx **out) {
     if (device < 0 || device >= n) return fail(nullptr, VTK_ERR_ARG, "vtk_ctx_create: bad device ordinal");
     auto *c = new vtk_ctx();
     c->device = device;
+    tune_from_env(c->tune);   // the only place the library reads its environment
     auto bad = [&](hipError_t e) {
         set_context_free_error(std::string("vtk_ctx_create: ") + hipGetErrorString(e));
         vtk_ctx_destroy(c);
@@ -1475,10 +1561,9 @@ int vtk_comm_unique_id(void *out128) {
 int vtk_comm_init(vtk_ctx *c, int rank, int world, const void *uid) {
     if (!c || world < 1 || rank < 0 || rank >= world) return fail(c, VTK_ERR_ARG, "vtk_comm_init: bad rank/world");
     HIPCHK(c, hipSetDevice(c->device));
-    // world 1: no communicator, unless VTK_COMM_SOLO=1 asks for a one-rank RCCL communicator
+    // world 1: no communicator, unless tuning comm_solo (VTK_COMM_SOLO=1) asks for a one-rank RCCL communicator
     // that runs every distributed code path (halo plan and exchange, all-reduces, split lists)
-    const char *solo = std::getenv("VTK_COMM_SOLO");
-    const bool force = world == 1 && solo && solo[0] == '1';
+    const bool force = world == 1 && c->tune.comm_solo;
     if (world == 1 && !force) { c->rank = 0; c->world = 1; c->dist = false; return VTK_OK; }
     if (!uid) return fail(c, VTK_ERR_ARG, "vtk_comm_init: unique id required");
     ncclUniqueId id;
@@ -1573,6 +1658,8 @@ int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t
             return fail(c, VTK_ERR_ARG, "vtk_csr_create: column index out of range");
     }
     TRY(finish_csr(A));
+    // the drop-in path gets the fast solver too: the 2D Vlasov structure is found in the CSR
+    TRY(auto_line_band(A));
     *out = A;
     A = nullptr;
     return VTK_OK;
@@ -1958,8 +2045,8 @@ int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len) {
     const int rc = band_check_all(A, line_len);
     if (rc == VTK_ERR_ARG)
         return fail(c, VTK_ERR_ARG, "vtk_csr_set_line_band: not a line-band operator for this line length "
-                                    "(line_len | n, >= 3 lines, every column in lines x-1..x+1; across ranks: "
-                                    "slabs of whole lines whose halo is the two neighbour lines)");
+                                    "(line_len | n, >= 3 lines, every column in lines x-1..x+1, n + 2 line_len "
+                                    "< 2^30; across ranks: slabs of whole lines whose halo is the two neighbour lines)");
     TRY(rc);
     A->band_L = line_len;
     return VTK_OK;
@@ -1979,7 +2066,23 @@ int vtk_csr_get_line_values(vtk_csr *A, int *separable) {
 
 int vtk_gmres_set_band(vtk_ctx *c, int on) {
     if (!c) return fail(nullptr, VTK_ERR_ARG, "vtk_gmres_set_band: ctx is NULL");
-    c->band = on != 0;
+    c->tune.band = on != 0;
+    return VTK_OK;
+}
+
+int vtk_ctx_set_tuning(vtk_ctx *c, const char *key, int value) {
+    if (!c) return fail(nullptr, VTK_ERR_ARG, "vtk_ctx_set_tuning: ctx is NULL");
+    const TuneKey *k = tune_key(key);
+    if (!k) return fail(c, VTK_ERR_ARG, std::string("vtk_ctx_set_tuning: unknown key ") + (key ? key : "(null)"));
+    c->tune.*k->mem = value;
+    return VTK_OK;
+}
+
+int vtk_ctx_get_tuning(vtk_ctx *c, const char *key, int *value) {
+    if (!c || !value) return fail(c, VTK_ERR_ARG, "vtk_ctx_get_tuning: NULL argument");
+    const TuneKey *k = tune_key(key);
+    if (!k) return fail(c, VTK_ERR_ARG, std::string("vtk_ctx_get_tuning: unknown key ") + (key ? key : "(null)"));
+    *value = c->tune.*k->mem;
     return VTK_OK;
 }
 

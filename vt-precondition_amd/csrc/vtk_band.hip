@@ -660,14 +660,13 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
 
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s, int canon) {
+                           hipStream_t s, int canon, int grid_cap) {
     if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || (halo && lblk < 0)) return hipErrorInvalidValue;
     const int64_t nch = (n + 63) / 64;
-    // 8192 workgroups (C3 line solve, in-process A/B: 8.69 ms vs 8.73 at 2048 and 8.85 with one
-    // chunk per wave; an XCD swizzle of the chunks 8.81 vs 8.70); VTK_LSV_SPMV_CAP overrides (A/B,
-    // read per launch)
-    int64_t cap = 8192;
-    if (const char *e = std::getenv("VTK_LSV_SPMV_CAP"); e && std::atoll(e) > 0) cap = std::atoll(e);
+    // grid_cap: 8192 workgroups by default (vtk::Tuning::lsv_spmv_cap; C3 line solve, in-process
+    // A/B: 8.69 ms vs 8.73 at 2048 and 8.85 with one chunk per wave; an XCD swizzle of the chunks
+    // 8.81 vs 8.70)
+    const int64_t cap = grid_cap > 0 ? grid_cap : 8192;
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>((nch + 3) / 4, cap));
     if (canon && halo) hipLaunchKernelGGL((k_lsv_spmv<true, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
     else if (canon) hipLaunchKernelGGL((k_lsv_spmv<false, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);

@@ -115,6 +115,27 @@ struct LineOp {
     double *ac = nullptr;
     int compact = 0;
 };
+
+// Tuning switches of a context (vtk_ctx_set_tuning): the defaults are the
+// production path, the others exist for in-process A/B measurements and the bit-identity tests
+// (the same sums with and without a byte-saving form).  Initialised from VTK_<KEY> (upper case)
+// once, at vtk_ctx_create -- never read per launch.
+struct Tuning {
+    int band = 1;             // line-band DCGS2 step allowed (vtk_gmres_set_band)
+    int band_lsv = 1;         // solver launches read the line-separable values (else SELL values)
+    int sell_canon = 1;       // ... and canonical rows' columns from the line index (no codes)
+    int band_canon = 1;       // the band step reads no codes on canonical rows
+    int band_canon_sl = 1;    // ... with the straight-line SpMV per line order
+    int sell_pad = 1;         // pad nearly uniform SELL widths (<= 2 % more entries)
+    int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
+    int plain_grid = 2048;    // workgroups of the plain SELL SpMV
+    int lsv_spmv_cap = 8192;  // workgroups of the line path's table SpMV
+    int ev_every = 1;         // host throttle event every this many Arnoldi steps (1..LOOKAHEAD+1)
+    int prof_perj = 0;        // profile class per band step index (band_step_jNN)
+    int debug_band = 0;       // band-check trace on stderr
+    int comm_solo = 0;        // vtk_comm_init with world 1 builds a one-rank RCCL communicator
+    int auto_band = 1;        // vtk_csr_create detects the line band (drop-in path)
+};
 }  // namespace vtk
 
 struct vtk_ctx {
@@ -130,7 +151,7 @@ struct vtk_ctx {
     bool host_comm = false;               // host-staged hooks (vtk_comm_init_host)
     vtk_host_comm hops{};
     int orth = VTK_ORTH_AUTO;
-    bool band = true;                     // line-band DCGS2 step allowed (vtk_gmres_set_band)
+    vtk::Tuning tune;                     // A/B switches (vtk_ctx_set_tuning), env at creation
     int n_cu = 0;                         // compute units (band step grid)
     // scratch shared by calls on this context
     double *d_part = nullptr;        // [8][GMAX] partial sums
@@ -231,6 +252,7 @@ struct SpmvIn {
     const double *lsv = nullptr;
     int lsv_L = 0, lsv_lblk = -1;
     int lsv_canon = 0;   // ... and every row canonical: k_sell computes the columns (canon_row)
+    int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX; vtk::Tuning)
 };
 
 LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);
@@ -414,7 +436,7 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
 // k_sell's plain SpMV, the same bits.  halo != null: the distributed layout (lblk the left block)
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s, int canon = 0);   // canon: rows canonical, no codes read
+                           hipStream_t s, int canon, int grid_cap);   // canon: rows canonical, no codes read
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 

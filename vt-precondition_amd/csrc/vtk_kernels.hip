@@ -978,14 +978,8 @@ size_t sell_scan_bytes(int64_t n) {
         else hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_, BS_, TRI_>), g, blk, 0, s, a);          \
     } while (0)
 
-// workgroups of the plain SELL SpMV (no partials: free of GMAX); VTK_PLAIN_GRID for tuning
-static inline int plain_grid() {
-    static const int g = [] {
-        const char *e = std::getenv("VTK_PLAIN_GRID");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 2 * GMAX;
-    }();
-    return g;
-}
+// workgroups of the plain SELL SpMV (no partials: free of GMAX); vtk::Tuning::plain_grid
+static inline int plain_grid(const SpmvIn &in) { return in.plain_grid > 0 ? in.plain_grid : 2 * GMAX; }
 static inline int sell_wu(const SpmvIn &in) {
     if (!VTK_SELL_WU || !VTK_SELL_UNIFORM || !in.sell || !in.groups) return 0;
     const int w = in.sell->uniform_w;
@@ -1063,7 +1057,7 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
     if (epi == EPI_PLAIN) {
         // no partials: SELL fills the chip at its 8 waves/SIMD (52 VGPRs) with 2048 workgroups
         // (tools/probe_sell.hip, C4: 965 us at 2048 vs 1362 us at 1024; C3 within 2 %)
-        const dim3 gp(sell ? (unsigned)std::max(1, std::min(in.groups->count, plain_grid())) : g.x);
+        const dim3 gp(sell ? (unsigned)std::max(1, std::min(in.groups->count, plain_grid(in))) : g.x);
         const int wu = sell_wu_plain(in);
         if (sell && wu == 9) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false, 0, 9>), gp, blk, 0, s, a);
         else if (sell) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false>), gp, blk, 0, s, a);

@@ -150,6 +150,32 @@ class Context:
         check(lib().vtk_gmres_set_orth(self._h, int(orth)), self._h)
         self.orth = int(orth)
 
+    def set_tuning(self, key: str, value: int):
+        """A/B and test switch of this context (``vtk_ctx_set_tuning``; keys in
+        include/vtkrylov.h).  Seeded from ``VTK_<KEY>`` when the context was created."""
+        check(lib().vtk_ctx_set_tuning(self._h, key.encode(), int(value)), self._h)
+
+    def get_tuning(self, key: str) -> int:
+        v = C.c_int()
+        check(lib().vtk_ctx_get_tuning(self._h, key.encode(), C.byref(v)), self._h)
+        return v.value
+
+    def tuning(self, **kv):
+        """``with ctx.tuning(band_lsv=0): ...`` -- set switches for a block, then restore."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_tuning(k) for k in kv}
+            try:
+                for k, v in kv.items():
+                    self.set_tuning(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_tuning(k, v)
+        return cm()
+
     band = True
 
     def set_band(self, on: bool):
@@ -296,11 +322,25 @@ def _is_device(a) -> bool:
     return getattr(a, "is_cuda", False) is True
 
 
-def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
+def _apply_line_len(A: CsrOperator, line_len):
+    """line_len None: keep what vtk_csr_create detected (the 2D Vlasov x-lines are found in
+    the CSR itself); 0: no line band; L: require the line band of L rows (ValueError if the
+    operator does not have it)."""
+    if line_len is None:
+        return A
+    if int(line_len) != A.line_band:
+        A.set_line_band(int(line_len))
+    return A
+
+
+def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None, line_len=None) -> CsrOperator:
     """Build a device CSR operator from ``(data, indices, indptr)`` or a SciPy sparse matrix.
 
     With ``offsets`` (world+1 row boundaries) the arrays are this rank's row block with
-    global column indices (multi-GPU); otherwise the whole matrix."""
+    global column indices (multi-GPU); otherwise the whole matrix.  The library looks for the
+    x-line structure of the 2D Vlasov operators in the CSR (``line_len=None``, the default) and
+    then runs the same fused solver as for a generated operator; ``line_len=0`` turns that off,
+    an explicit ``line_len`` requires it (see :meth:`CsrOperator.set_line_band`)."""
     ctx = ctx or default_context()
     if hasattr(arg, "tocsr"):
         # stored order kept: csr_matvec sums each row in stored order, so must the device
@@ -329,28 +369,43 @@ def csr_matrix(arg, shape=None, *, ctx: Context | None = None, offsets=None) -> 
         torch.cuda.current_stream(data.device).synchronize()
         nnz = int(indptr[-1].item())   # the CSR may carry spare capacity beyond indptr[-1]
         offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
+        # the library copies nnz entries device to device: never past the tensors' ends
+        n_rows = int(shape[0]) if offs is None else int(offs[ctx.rank + 1] - offs[ctx.rank])
+        if indptr.numel() != n_rows + 1:
+            raise ValueError(f"csr_matrix: indptr has {indptr.numel()} entries, expected {n_rows + 1}")
+        if nnz < 0 or nnz > indices.numel() or nnz > data.numel():
+            raise ValueError(f"csr_matrix: indptr[-1] = {nnz} exceeds the {indices.numel()} indices / "
+                             f"{data.numel()} values given")
         h = C.c_void_p()
         check(lib().vtk_csr_create(ctx.handle, int(shape[0]), None if offs is None else _np_ptr(offs),
                                    nnz, C.c_void_p(indptr.data_ptr()),
                                    C.c_void_p(indices.data_ptr()), C.c_void_p(data.data_ptr()),
                                    int(fp32), _abi.PTR_DEVICE, C.byref(h)), ctx.handle)
-        return CsrOperator(h, ctx, fp32)
+        return _apply_line_len(CsrOperator(h, ctx, fp32), line_len)
     data = np.asarray(data)
     fp32 = data.dtype == np.float32
     data = np.ascontiguousarray(data, dtype=np.float32 if fp32 else np.float64)
     indices = np.ascontiguousarray(indices, dtype=np.int32)
     indptr = np.ascontiguousarray(indptr, dtype=np.int32)
     offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
+    nnz = int(indptr[-1])
+    n_rows = int(shape[0]) if offs is None else int(offs[ctx.rank + 1] - offs[ctx.rank])
+    if indptr.shape[0] != n_rows + 1:
+        raise ValueError(f"csr_matrix: indptr has {indptr.shape[0]} entries, expected {n_rows + 1}")
+    if nnz < 0 or nnz > indices.shape[0] or nnz > data.shape[0]:
+        raise ValueError(f"csr_matrix: indptr[-1] = {nnz} exceeds the {indices.shape[0]} indices / "
+                         f"{data.shape[0]} values given")
     h = C.c_void_p()
     check(lib().vtk_csr_create(ctx.handle, int(shape[0]), None if offs is None else _np_ptr(offs),
-                               int(indptr[-1]), _np_ptr(indptr), _np_ptr(indices), _np_ptr(data),
+                               nnz, _np_ptr(indptr), _np_ptr(indices), _np_ptr(data),
                                int(fp32), _abi.PTR_HOST, C.byref(h)), ctx.handle)
-    return CsrOperator(h, ctx, fp32)
+    return _apply_line_len(CsrOperator(h, ctx, fp32), line_len)
 
 
-def load_npz(file, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
+def load_npz(file, *, ctx: Context | None = None, offsets=None, line_len=None) -> CsrOperator:
     """``scipy.sparse.load_npz`` for CSR archives, straight to the device: with ``offsets``
-    (world+1 row boundaries) each rank reads only its row block (``ctx.rank``)."""
+    (world+1 row boundaries) each rank reads only its row block (``ctx.rank``).  ``line_len``
+    as in :func:`csr_matrix`."""
     from .npz import load_npz_arrays
     ctx = ctx or default_context()
     rows = None
@@ -360,7 +415,7 @@ def load_npz(file, *, ctx: Context | None = None, offsets=None) -> CsrOperator:
             raise ValueError("offsets must have world+1 entries")
         rows = (int(offs[ctx.rank]), int(offs[ctx.rank + 1]))
     indptr, indices, data, shape = load_npz_arrays(file, rows)
-    return csr_matrix((data, indices, indptr), shape=shape, ctx=ctx, offsets=offsets)
+    return csr_matrix((data, indices, indptr), shape=shape, ctx=ctx, offsets=offsets, line_len=line_len)
 
 
 def save_npz(file, A: CsrOperator, compressed: bool = True) -> None:

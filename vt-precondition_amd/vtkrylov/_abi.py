@@ -8,6 +8,7 @@ library is missing or no HIP device is visible, calls fail loudly.
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -54,6 +55,9 @@ I64P = C.POINTER(C.c_int64)
 # name -> (restype, argtypes); must cover every function declared in include/vtkrylov.h
 PROTOTYPES = {
     "vtk_abi_version": (C.c_int, []),
+    "vtk_build_id": (C.c_char_p, []),
+    "vtk_ctx_set_tuning": (C.c_int, [P, C.c_char_p, C.c_int]),
+    "vtk_ctx_get_tuning": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
     "vtk_status_string": (C.c_char_p, [C.c_int]),
     "vtk_last_error": (C.c_int, [P, C.c_char_p, C.c_size_t]),
     "vtk_vlasov_size": (C.c_int, [C.POINTER(VlasovParams), I64P, I64P]),
@@ -107,7 +111,7 @@ PROTOTYPES = {
 }
 
 
-ABI_VERSION = 4   # include/vtkrylov.h VTK_ABI_VERSION
+ABI_VERSION = 5   # include/vtkrylov.h VTK_ABI_VERSION
 
 
 class BandGeometry(C.Structure):
@@ -156,6 +160,47 @@ def lib() -> C.CDLL:
             raise ImportError("libvtkrylov.so ABI version mismatch")
         _lib = L
     return _lib
+
+
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "vtkrylov.h")
+
+
+def source_build_id(csrc: str = CSRC, header: str = HEADER, extra: str = "") -> str | None:
+    """The build id csrc/Makefile compiles into vtk_build_id(): SHA-256 (16 hex digits) of the
+    .hip/.hpp/.cpp sources in name order, the public header, the Makefile and EXTRA.  None when
+    the sources are not present."""
+    if not os.path.isdir(csrc) or not os.path.exists(header):
+        return None
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".hpp", ".cpp")))
+    h = hashlib.sha256()
+    for path in [os.path.join(csrc, f) for f in names] + [header, os.path.join(csrc, "Makefile")]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(extra.encode())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    return lib().vtk_build_id().decode()
+
+
+class StaleBuildError(RuntimeError):
+    pass
+
+
+def check_build_id(built: str | None = None, sources: str | None = None) -> str:
+    """Raise StaleBuildError when the loaded libvtkrylov.so was not built from the checked-out
+    sources (the GPU box runs the binary pushed from the build container).  An explicit VTK_LIB
+    (A/B builds of other variants) is not checked.  Returns the build id."""
+    built = build_id() if built is None else built
+    if os.environ.get("VTK_LIB") and built is not None:
+        return built
+    sources = source_build_id() if sources is None else sources
+    if sources is not None and built != sources:
+        raise StaleBuildError(f"libvtkrylov.so build id {built} does not match the sources ({sources}): "
+                              "rebuild with __graft_entry__.build() / make -C vt-precondition_amd/csrc")
+    return built
 
 
 def last_error(ctx=None) -> str:
