@@ -95,3 +95,44 @@ def test_step_main_line_jacobi(gpu, tmp_path, name):
     ref = coracle.gmres(ip, ix, d, b, coracle.line_setup(ip, ix, d, p.shape[1], 25), rtol=1e-8)
     assert abs(res["solve"]["inner_iters"] - ref.inner_iters) <= 1
     assert np.linalg.norm(b - coracle.spmv(ip, ix, d, step.x)) <= 1e-8 * np.linalg.norm(b)
+
+
+@pytest.mark.gpu
+def test_step_main_npz_2d_runs_band_step(gpu, tmp_path):
+    """operator/file of a 2D Vlasov archive: the step's load_npz finds the x-line structure
+    (operator/line_len auto) and the solve runs the fused band step, as a generated operator's
+    does; line_jacobi takes the detected line length as its stride."""
+    from oracle import coracle, twin
+    from vtkrylov import npz
+    from vtsetup.krylov_precondition import KrylovPrecondition
+    p = twin.CONFIGS["C1"]
+    ip, ix, d = coracle.generate(p)
+    f = tmp_path / "c1.npz"
+    npz.save_npz_arrays(f, ip, ix, d, (p.n, p.n))
+    cfg = SolverConfig.load(config="C1", report=str(tmp_path / "r.json"), operator_file=str(f))
+    assert cfg.line_len is None
+    res = KrylovPrecondition(cfg, ctx=gpu).main()
+    assert res["operator"]["line_band"] == p.shape[1] and res["operator"]["line_values"] == 2
+    assert res["solve"]["info"] == 0 and res["solve"]["band_step"]
+    cfg0 = SolverConfig.load(config="C1", report=str(tmp_path / "r0.json"), operator_file=str(f), line_len=0)
+    res0 = KrylovPrecondition(cfg0, ctx=gpu).main()
+    assert res0["operator"]["line_band"] == 0 and not res0["solve"]["band_step"]
+    assert abs(res0["solve"]["inner_iters"] - res["solve"]["inner_iters"]) <= 1
+    cfgl = SolverConfig.load(config="C1", report=str(tmp_path / "rl.json"), operator_file=str(f),
+                             preconditioner="line_jacobi")
+    resl = KrylovPrecondition(cfgl, ctx=gpu).main()
+    assert resl["preconditioner"]["line_stride"] == p.shape[1] and resl["solve"]["info"] == 0
+
+
+def test_line_len_node(tmp_path):
+    """operator/line_len: 'auto' (or absent) -> None, an integer -> that line length."""
+    import shutil
+    from vtsetup.config import DEFAULT_XML
+    assert SolverConfig.load().line_len is None
+    x = tmp_path / "c.xml"
+    shutil.copy(DEFAULT_XML, x)
+    s = x.read_text().replace("<line_len>auto</line_len>", "<line_len>800</line_len>")
+    x.write_text(s)
+    assert SolverConfig.load(str(x)).line_len == 800
+    x.write_text(s.replace("<line_len>800</line_len>", ""))
+    assert SolverConfig.load(str(x)).line_len is None

@@ -79,7 +79,7 @@ struct TuneKey { const char *name; int Tuning::*mem; };
 constexpr TuneKey TUNE_KEYS[] = {
     {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
     {"band_canon", &Tuning::band_canon}, {"band_canon_sl", &Tuning::band_canon_sl},
-    {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid},
+    {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
 };
@@ -340,6 +340,7 @@ SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nu
         in.groups = g ? g : &A->g_all;
     }
     in.plain_grid = A->ctx->tune.plain_grid;
+    in.swz = A->ctx->tune.sell_swz;
     return in;
 }
 
@@ -918,6 +919,11 @@ struct Solver {
     // (step j's w in the buffer j % 3: the band step reads w_{j-1} and w_j, writes w_{j+1})
     bool band = false;
     int band_G = 0, band_H = 1;
+    int band_G3 = 0;   // grid of the three-workgroups-per-CU launches (band_opt bit 1, j <= BAND_J3)
+    // workgroups (= partials) of the band step launched at step j
+    int band_grid(int j, int opt, int j3) const {
+        return (opt & 2) && j <= std::min(j3, BAND_J3) && band_G3 > 0 ? band_G3 : band_G;
+    }
     double *w3 = nullptr;
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
 };
@@ -1041,7 +1047,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *const wb[3] = {s.w, s.tmp, s.w3};
         double *w_cur = band ? wb[j % 3] : s.w;
         if (band && j > 0) {
-            cnt = s.band_G;
+            cnt = s.band_grid(j - 1, s.ghost ? 0 : c->tune.band_opt, c->tune.band_j3);
         } else if (fused && bj_split(s.M)) {
             // interior tiles while the halo is in flight, boundary tiles once it has landed;
             // their partials side by side (cnt = both grids)
@@ -1151,7 +1157,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.left_blk = s.A->band_lblk;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
             a.canon = band_lsv && s.A->lsv_canon && band_canon ? (canon_sl ? 2 : 1) : 0;
-            HIPCHK(c, launch_band_step(a, s.band_G, s.A->sell.uniform_w, c->stream));
+            a.opt = s.ghost ? 0 : c->tune.band_opt;   // variants exist for the one-rank instantiation
+            a.j3 = std::min(c->tune.band_j3, BAND_J3);
+            HIPCHK(c, launch_band_step(a, s.band_grid(j, a.opt, a.j3), s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
             HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
@@ -1214,6 +1222,10 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             band_R = g.ranges;
             s.band_H = g.parts;
             s.band_G = band_R * g.parts;
+            // three workgroups per CU for the low-j steps: 1.5x the line ranges (>= 2 lines each)
+            const int64_t R3 = std::min<int64_t>({std::max<int64_t>(1, 3LL * (c->n_cu > 0 ? c->n_cu : 256) / g.parts),
+                                                  g.lines / 2, (int64_t)GMAX / g.parts});
+            s.band_G3 = (int)R3 * g.parts;
         }
     }
     // every rank takes the same path: the band step exchanges ghost lines with its neighbours

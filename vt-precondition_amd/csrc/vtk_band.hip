@@ -69,8 +69,18 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 // couplings per line) instead of the SELL copy's 5 values per row; VMODE 2 (also canonical
 // rows, vtk_csr::lsv_canon): the entries' kinds and order from canon_order instead of the SELL
 // codes and dictionary.  The same values in the same order either way
-template <int WU, int J, int GEO, int VMODE = 0, bool GH = true>
-__global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(4))) void k_band_step(BandK a) {
+// OPT bit 0 (SPF): with the next-line prefetch (J <= VTK_BAND_PF) and canonical rows, the SpMV
+// operands of a line (D, m, the line's v couplings) travel in the same prefetch as the update
+// operands, one line ahead.  Loaded at the head of their own iteration they made the wait for the
+// prefetched update operands a wait for everything (s_waitcnt vmcnt(0): the loads sit in
+// exec-masked blocks, so the counter cannot be tracked per load): one exposed memory round trip
+// per line.
+// OPT bit 1 (WPC3): registers capped for 3 workgroups per CU (6 waves per SIMD) -- the low-J
+// launches, whose LDS (ring + (J + 1) staged basis rows) leaves room for a third workgroup and
+// whose serial line walks are latency-bound; the host plans 1.5x the line ranges for them.
+template <int OPT> constexpr int band_wpe() { return (OPT & 2) ? 6 : 4; }
+template <int WU, int J, int GEO, int VMODE = 0, bool GH = true, int OPT = 0>
+__global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(band_wpe<OPT>()))) void k_band_step(BandK a) {
     constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
     __shared__ double vbuf[VTK_BAND_REREAD ? 1 : (VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
@@ -125,15 +135,34 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     // operands are loaded during this line's SpMV and dots.  (A partial prefetch of 4 basis rows
     // for larger J measured slower: 1234 vs 1254 it/s, spills)
     constexpr bool PF = J <= VTK_BAND_PF;
+    constexpr bool SPF = PF && CANON && (OPT & 1);
     // update operands of iteration it's line on the lane's row: V_k (k < j), w_{j-1} (j = 0: v_0)
     // and w_j
     struct Ld {
         double v[J > 0 ? J : 1];
         double wm, wj;
+        double drow, mrow, tv0, tv1;   // SPF: the SpMV operands of the iteration's line x
     };
     auto load = [&](int it, Ld &o) {
         int kind;
         const int y = line_of(it, kind);
+        if constexpr (SPF) {
+            // line x = y - 1 of iteration it (owned when it >= 2): D, m on the lane's row, the
+            // line's v couplings (the same loads the iteration head issues without SPF)
+            o.drow = 0.0;
+            o.mrow = 1.0;
+            o.tv0 = o.tv1 = 0.0;
+            if (it >= 2) {
+                const int xs = xa - 2 + it;
+                const int64_t rs = (int64_t)xs * L + (own ? v : v0);
+                if (own) {
+                    o.drow = __builtin_nontemporal_load(a.lsv + rs);
+                    o.mrow = __builtin_nontemporal_load(a.mtri + rs);
+                }
+                o.tv0 = a.lsv[a.n + 2 * L + xs];
+                o.tv1 = a.lsv[a.n + 2 * L + X + xs];
+            }
+        }
         const int64_t row = (int64_t)y * L + (upd ? v : 0);
         o.wm = 0.0;
         o.wj = 0.0;
@@ -223,7 +252,7 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         int dv = 0;
         double d[LSV ? 1 : WU];
         double mrow = 1.0, drow = 0.0, tv0 = 0.0, tv1 = 0.0;
-        if (work) {
+        if (work && !SPF) {
             if constexpr (!CANON) {
                 word = __builtin_nontemporal_load(a.pk + q * 64 + l64);
                 const int64_t qd = q0 + (lane >> 4);
@@ -244,6 +273,12 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
             Ld cu;
             if constexpr (PF) cu = nx;
             else load(it, cu);
+            if constexpr (SPF) {
+                drow = cu.drow;
+                mrow = cu.mrow;
+                tv0 = cu.tv0;
+                tv1 = cu.tv1;
+            }
             const double pn = update(it, cu);
             if (upd) ring[slot(y) + tid] = pn;
             if constexpr (PF) {
@@ -412,6 +447,19 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     }
 }
 
+// the one-rank production instantiations (canonical rows, line-separable values) with the
+// variant bits of a.opt; WPC3 only where the LDS of three workgroups fits (J <= BAND_J3)
+template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipStream_t s) {
+    const dim3 g(grid), blk(BandGeo<VTK_BAND_GEO>::T);
+    if constexpr (J <= BAND_J3) {
+        if (J > a.j3) {}
+        else if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false, 3>), g, blk, 0, s, a); return; }
+        if ((a.opt & 3) == 2) { hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false, 2>), g, blk, 0, s, a); return; }
+    }
+    if (a.opt & 1) hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false, 1>), g, blk, 0, s, a);
+    else hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false>), g, blk, 0, s, a);
+}
+
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     constexpr int lp = BandGeo<VTK_BAND_GEO>::LP;
     if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > lp || (a.L / a.H_parts) % 8 != 0 ||
@@ -421,7 +469,7 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     switch (a.j) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
-        if (a.lsv && a.canon && VTK_BAND_GHT && !a.ghost) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2, false>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        if (a.lsv && a.canon && VTK_BAND_GHT && !a.ghost) launch_band_one_rank<J_>(a, grid, s); \
         else if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 1>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
         else hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \

@@ -129,6 +129,9 @@ struct Tuning {
     int sell_pad = 1;         // pad nearly uniform SELL widths (<= 2 % more entries)
     int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
     int plain_grid = 2048;    // workgroups of the plain SELL SpMV
+    int sell_swz = 0;         // SELL launches walk their groups in XCD-contiguous order
+    int band_opt = 0;         // band step variant bits (vtk_band.hip k_band_step OPT)
+    int band_j3 = 2;          // ... bit 1 (three workgroups per CU) for steps j <= band_j3
     int lsv_spmv_cap = 8192;  // workgroups of the line path's table SpMV
     int ev_every = 1;         // host throttle event every this many Arnoldi steps (1..LOOKAHEAD+1)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
@@ -253,6 +256,7 @@ struct SpmvIn {
     int lsv_L = 0, lsv_lblk = -1;
     int lsv_canon = 0;   // ... and every row canonical: k_sell computes the columns (canon_row)
     int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX; vtk::Tuning)
+    int swz = 0;         // XCD-aware SELL group order (vtk::Tuning::sell_swz)
 };
 
 LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);
@@ -411,11 +415,16 @@ struct BandK {
     const double *lsv;           // line-separable values (vtk_csr::d_lsv) or null: SELL values
     int canon;                   // with lsv: canonical rows (vtk_csr::lsv_canon), no codes read;
                                  // 2: the SpMV as straight-line code per line order
+    int opt = 0;                 // kernel variant bits (vtk::Tuning::band_opt; vtk_band.hip OPT)
+    int j3 = 0;                  // opt bit 1 applies to steps j <= j3 (<= BAND_J3)
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
 // geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
 // line (one part; parts per line = band_parts), BAND_WPC workgroups per CU (LDS-bound)
 constexpr int BAND_LP = 400, BAND_T = 448, BAND_WPC = 2;
+// band steps j <= BAND_J3 may run three workgroups per CU (Tuning::band_opt bit 1): their LDS
+// (ring + (j + 1) staged basis rows of BAND_LP doubles) fits three times into 160 KB
+constexpr int BAND_J3 = 4;   // (instantiated up to here; beyond j = 2 the 80-VGPR cap spills)
 // vectors per ghost line and step of the distributed band step: v_{j-1} (v_0 at j = 0), w_j
 constexpr int BAND_GHOST_VECS = 2;
 hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,

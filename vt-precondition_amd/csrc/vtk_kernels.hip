@@ -65,6 +65,7 @@ struct SpmvK {
     const double *lsv;
     int lsv_L, lsv_lblk;
     int canon;   // with lsv: every row canonical (vtk_csr::lsv_canon): columns from canon_row
+    int swz;     // XCD-aware group order (xcd_swizzle; vtk::Tuning::sell_swz)
 };
 
 // value of entry (row, c) from the line-separable tables; drow = D[row], (xl, v) the row's line
@@ -462,7 +463,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
 #pragma unroll
         for (int k = 0; k < JB; ++k) { as_[k] = 0.0; az_[k] = 0.0; }
     }
-    const int t0 = VTK_SELL_SWZ ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int t0 = (VTK_SELL_SWZ || a.swz) ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     // PIPE (compile-time widths): the next chunk's code words, dictionary, values and own-row
     // operands are loaded while this chunk's gathers are in flight -- issued right after them,
     // so waiting for the gathers does not wait for the prefetch -- and consumed one iteration
@@ -1041,7 +1042,7 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
                       sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0,
                       sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk,
-                      sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0};
+                      sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0, in.swz};
     return a;
 }
 

@@ -34,6 +34,11 @@ class Etree:
     def dict_walkData(self, attrib: str) -> dict:
         return {n.tag: (n.text or "").strip() for n in self._find(attrib)}
 
+    def get_optional(self, attrib: str, default=None):
+        """get_node_value for nodes a configuration may leave out (None / default when absent)."""
+        node = self.root.find(f".//{attrib}")
+        return default if node is None else (node.text or "").strip()
+
 
 def parse_config_spec(spec: str):
     """'2:1250x800:f64' -> (dim, shape, fp32)"""
@@ -67,6 +72,7 @@ class SolverConfig:
     seed: int
     device: int
     report: str
+    line_len: int | None = None   # operator/line_len: None (absent / "auto") = detected by vtk_csr_create
 
     @classmethod
     def load(cls, path: str = DEFAULT_XML, **overrides) -> "SolverConfig":
@@ -91,6 +97,8 @@ class SolverConfig:
                   seed=int(t.get_node_value("rhs/seed"), 0),
                   device=int(t.get_node_value("run/device")),
                   report=t.get_node_value("run/report"))
+        ll = t.get_optional("operator/line_len", "auto").lower()
+        cfg.line_len = None if ll in ("", "auto") else int(ll)
         for k, v in overrides.items():
             if v is not None:
                 setattr(cfg, k, v)

@@ -32,12 +32,18 @@ class KrylovPrecondition:
         self.ctx = self.ctx or vk.Context(c.device)
         t = time.perf_counter()
         if c.operator_file:
-            self.A = vk.load_npz(c.operator_file, ctx=self.ctx)
+            # the x-line structure of a 2D Vlasov archive is found by the library (line_len None)
+            # and runs the fused band step, as a generated operator does; operator/line_len
+            # requires (L) or refuses (0) it
+            self.A = vk.load_npz(c.operator_file, ctx=self.ctx, line_len=c.line_len)
         else:
             p = vk.vlasov_params(c.dim, c.shape, fp32=c.fp32, **c.physics)
             self.A = vk.vlasov_operator(p, ctx=self.ctx)
+            if c.line_len is not None and c.line_len != self.A.line_band:
+                self.A.set_line_band(c.line_len)
         self.result["operator"] = {"n": self.A.n_global, "nnz": self.A.nnz,
                                    "source": c.operator_file or f"vlasov {c.config}",
+                                   "line_band": self.A.line_band, "line_values": self.A.line_values,
                                    "t_assemble_s": time.perf_counter() - t}
 
     def setup_preconditioner(self):
@@ -52,8 +58,13 @@ class KrylovPrecondition:
             stride = c.line_stride
             if stride <= 0:
                 if c.operator_file:
-                    raise ValueError("line_jacobi on an operator file needs preconditioner/line_stride")
-                stride = vk.vlasov_line_stride(vk.vlasov_params(c.dim, c.shape))
+                    # the detected x-line length is the line stride of a 2D operator
+                    stride = self.A.line_band
+                    if stride <= 0:
+                        raise ValueError("line_jacobi on an operator file without a detected x-line "
+                                         "structure needs preconditioner/line_stride")
+                else:
+                    stride = vk.vlasov_line_stride(vk.vlasov_params(c.dim, c.shape))
             self.M = vk.line_jacobi(self.A, stride, c.line_segment)
             info.update(line_stride=stride, line_segment=c.line_segment)
         info["t_setup_s"] = time.perf_counter() - t
@@ -68,7 +79,7 @@ class KrylovPrecondition:
         st = vk.last_stats()
         self.result["solve"] = {"info": info, "inner_iters": st.inner_iters,
                                 "restarts": st.restarts, "rnorm": st.rnorm, "bnorm": st.bnorm,
-                                "t_solve_s": st.t_solve,
+                                "t_solve_s": st.t_solve, "band_step": bool(st.band),
                                 "iters_per_s": st.inner_iters / st.t_solve if st.t_solve else None}
 
     def report(self):
