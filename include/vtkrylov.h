@@ -170,7 +170,8 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
  * with and without a byte-saving form).  Each key is seeded from the environment variable
  * VTK_<KEY in upper case> once, when the context is created; the library reads its environment
  * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_canon_sl, sell_pad,
- * sell_grid, plain_grid, sell_swz, band_opt, band_j3, lsv_spmv_cap, ev_every, prof_perj, debug_band, comm_solo, auto_band.
+ * sell_grid, plain_grid, sell_swz, band_opt, band_j3, lsv_spmv_cap, ev_every, prof_perj, debug_band, comm_solo, auto_band, grid4,
+ * c4_fused.
  * VTK_ERR_ARG for an unknown key.  (ABI 5) */
 int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);
 int vtk_ctx_get_tuning(vtk_ctx *ctx, const char *key, int *value);
@@ -239,6 +240,18 @@ int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len);
  * order): the band step derives the entries' kinds and order from the row's line and reads no
  * column codes either.  ABI 4. */
 int vtk_csr_get_line_values(vtk_csr *A, int *separable);
+/* 4D phase-space grid: rows ((ix Ny + iy) Nvx + jvx) Nvy + jvy, x and y periodic,
+ * vx and vy Dirichlet, every row coupled to x+-1, y+-1, vx+-1, vy+-1 in ascending column order,
+ * each coupling's value depending on one coordinate (x: jvx, y: jvy, vx: ix, vy: iy) -- the 4D
+ * Vlasov operators.  Checked on the device bit for bit (VTK_ERR_ARG when it does not hold; Ny 0
+ * clears it); set automatically by vtk_csr_create_vlasov (dim 4) and by vtk_csr_create when the
+ * first row's column distances are 1, Nvy, Nvx Nvy, Ny Nvx Nvy.  With it the solver's SpMV
+ * launches take each row's columns from its coordinates and its values from the diagonal per row
+ * and per-coordinate tables (one value per row read instead of nine values and nine codes; the
+ * same sums).  Rank-local, not collective; across ranks the slabs must be whole x planes with the
+ * two neighbour planes as the halo.  dims = {Ny, Nvx, Nvy} (zeros: not set).  (ABI 5) */
+int vtk_csr_set_grid4(vtk_csr *A, int64_t Ny, int64_t Nvx, int64_t Nvy);
+int vtk_csr_get_grid4(vtk_csr *A, int64_t *dims);
 
 /* y = A x on this rank's rows; x holds this rank's rows of the vector (halo exchanged
  * internally over RCCL when world > 1).  Bit-identical to csr_matvec (serial row sums). */

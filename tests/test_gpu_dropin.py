@@ -65,8 +65,8 @@ def test_line_len_argument(vk_lib, gpu):
     assert s0.band == 0 and i0 == 0
     A1 = vk_lib.csr_matrix(S, ctx=gpu, line_len=p.shape[1])
     assert A1.line_band == p.shape[1]
-    with pytest.raises(ValueError):
-        vk_lib.csr_matrix(S, ctx=gpu, line_len=2 * p.shape[1])   # no such structure
+    with pytest.raises(ValueError):   # x couplings two half-lines away: no such structure
+        vk_lib.csr_matrix(S, ctx=gpu, line_len=p.shape[1] // 2)
     for o in (M0, A0, A1):
         o.close()
 
@@ -134,3 +134,81 @@ def test_device_csr_overlong_indptr_rejected(vk_lib, gpu):
         ip2 = ip.copy()
         ip2[-1] += 5
         vk_lib.csr_matrix((d, ix, ip2), shape=(p.n, p.n), ctx=gpu)
+
+
+def test_destroy_in_any_order(vk_lib):
+    """Finalisers of a reference cycle run in any order: a preconditioner destroyed after its
+    operator, and an operator after its context, must not touch the freed parent."""
+    import scipy.sparse as sp
+    p = twin.CONFIGS["S2"]
+    ip, ix, d = coracle.generate(p)
+    ctx = vk_lib.Context(0)
+    A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=ctx)
+    M = vk_lib.block_jacobi(A, 8)
+    L = vk_lib.line_jacobi(A, p.shape[1], 8)
+    A.close()
+    M.close()
+    L.close()
+    B = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=ctx)
+    ctx.close()
+    B.close()
+
+
+@pytest.mark.parametrize("name", ["S4", "S4F"])
+def test_grid4_rows_bit_identical(vk_lib, gpu, name):
+    """4D grid rows (vtk_csr_set_grid4): the solver's SELL launches take the columns
+    from the row's coordinates and the values from D and the per-coordinate tables -- the same
+    entries in the same order as the SELL copy, so x is bit-identical with the grid4 switch off;
+    the uploaded CSR is detected as a grid too."""
+    p = twin.CONFIGS[name]
+    G = vk_lib.vlasov_operator(vk_lib.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=gpu)
+    assert G.grid4 == tuple(p.shape[1:])
+    ip, ix, d = G.download()
+    U = vk_lib.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=gpu)
+    assert U.grid4 == tuple(p.shape[1:])
+    b = twin.rhs(p.n)
+    out = []
+    for A in (G, U):
+        M = vk_lib.block_jacobi(A, 8)
+        for orth in ("dcgs2", "mgs"):
+            x1, i1, s1 = _solve(vk_lib, A, M, b, orth=orth)
+            with gpu.tuning(grid4=0):
+                x0, i0, s0 = _solve(vk_lib, A, M, b, orth=orth)
+            with gpu.tuning(c4_fused=1):
+                x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)
+            assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
+            assert np.array_equal(x1, x0), "grid rows change the bits"
+            if orth == "mgs":
+                assert np.array_equal(x1, x2)
+            else:   # the fused dots sum in another fixed order: the DCGS2 bars
+                assert abs(s2.inner_iters - s1.inner_iters) <= 1
+                assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) < 1e-9
+            out.append(x1)
+        M.close()
+    assert np.array_equal(out[0], out[2]) and np.array_equal(out[1], out[3])
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    assert np.linalg.norm(out[1] - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    for o in (U, G):
+        o.close()
+
+
+def test_grid4_rejects_other_structures(vk_lib, gpu):
+    import scipy.sparse as sp
+    p = twin.CONFIGS["S4"]
+    ip, ix, d = coracle.generate(p)
+    A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    with pytest.raises(ValueError):
+        A.set_grid4(p.shape[1], p.shape[3], p.shape[2])   # swapped velocity extents
+    assert A.grid4 == tuple(p.shape[1:])                   # the detected structure is kept
+    A.set_grid4(0, 0, 0)
+    assert A.grid4 == (0, 0, 0)
+    d2 = d.copy()
+    d2[ip[7] + 1] *= 1.0 + 1e-6                             # one coupling no longer by-coordinate
+    B = vk_lib.csr_matrix(sp.csr_matrix((d2, ix, ip), shape=(p.n, p.n)), ctx=gpu)
+    assert B.grid4 == (0, 0, 0)
+    S2 = twin.CONFIGS["S2"]
+    q = coracle.generate(S2)
+    C2 = vk_lib.csr_matrix((q[2], q[1], q[0]), shape=(S2.n, S2.n), ctx=gpu)
+    assert C2.grid4 == (0, 0, 0) and C2.line_band == S2.shape[1]
+    for o in (A, B, C2):
+        o.close()

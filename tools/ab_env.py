@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--seg", type=int, default=25)
     ap.add_argument("--slab", type=int, default=1, help="one rank's x-slab at this many GPUs (as bench.py --slab)")
     ap.add_argument("--comm-solo", action="store_true", help="the distributed code path on one rank (bench.py --comm-solo)")
+    ap.add_argument("--perj", action="store_true", help="also one profiled solve per value: band step us per j")
+    ap.add_argument("--set", default="", help="fixed tuning for every value, e.g. band_j3=4,sell_swz=1")
     a = ap.parse_args()
     import vtkrylov as vk
     from oracle import twin
@@ -48,6 +50,9 @@ def main():
     b = torch.from_numpy(vk.rhs_splitmix(n)).to(torch.device("cuda", 0))   # device-resident, as bench.py
     torch.cuda.synchronize()
     key = a.env[4:].lower() if a.env.startswith("VTK_") else a.env
+    for kv in filter(None, a.set.split(",")):
+        k, v = kv.split("=")
+        ctx.set_tuning(k, int(v))
     vals = a.values.split(",")
     times = {v: [] for v in vals}
     iters = {}
@@ -61,7 +66,19 @@ def main():
             iters[v] = (st.inner_iters, st.band, info)
             if r > 0:   # round 0: warm-up
                 times[v].append(round(dt, 3))
-    out = {"config": a.config, "prec": a.prec, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,
+    perj = {}
+    if a.perj:
+        ctx.set_tuning("prof_perj", 1)
+        for v in vals:
+            ctx.set_tuning(key, int(v))
+            ctx.profile(True)
+            vk.gmres(A, b, rtol=a.rtol, M=M)
+            pr = ctx.profile_read()
+            ctx.profile(False)
+            perj[v] = {k: round(e["avg_us"], 1) for k, e in sorted(pr.items())
+                       if k.startswith("band_step") or k in ("dc_scalar", "dc_update", "spmv_resid_bj", "spmv_bj_dc")}
+        ctx.set_tuning("prof_perj", 0)
+    out = {"config": a.config, "set": a.set, "perj_us": perj, "prec": a.prec, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,
            "median_ms": {v: statistics.median(t) for v, t in times.items()}, "ms": times}
     print(json.dumps(out))
     M.close()

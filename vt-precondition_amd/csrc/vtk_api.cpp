@@ -82,6 +82,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused},
 };
 
 const TuneKey *tune_key(const char *name) {
@@ -360,6 +361,7 @@ bool lsv_on(const vtk_csr *A) {
            (!A->ctx->dist || A->band_ghost);
 }
 SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
+    if (in.sell && A->d_g4tab && A->ctx->tune.grid4) in.g4 = A->g4;   // 4D grid rows (Grid4)
     if (in.sell && lsv_on(A)) {
         in.lsv = A->d_lsv;
         in.lsv_L = (int)A->band_L;
@@ -373,6 +375,7 @@ double matrix_bytes(const vtk_csr *A);
 // matrix bytes a solver SELL launch reads (lsv_in)
 double solver_matrix_bytes(const vtk_csr *A) {
     const double b = matrix_bytes(A);
+    if (A->use_sell && A->d_g4tab && A->ctx->tune.grid4) return (A->fp32 ? 4.0 : 8.0) * (double)A->n_local;   // D only
     if (!lsv_on(A)) return b;
     if (A->lsv_canon && A->ctx->tune.sell_canon) return 8.0 * (double)A->n_local;   // the diagonal only
     return b - 8.0 * (double)A->sell.entries + 8.0 * (double)A->n_local;
@@ -660,7 +663,7 @@ int check_partition(vtk_ctx *c, int64_t n_global, const int64_t *offsets, std::v
 
 void destroy_csr(vtk_csr *A) {
     if (!A) return;
-    if (A->ctx) (void)hipSetDevice(A->ctx->device);
+    (void)hipSetDevice(A->device);
     (void)hipFree(A->d_indptr);
     (void)hipFree(A->d_indices);
     (void)hipFree(A->d_data);
@@ -669,6 +672,8 @@ void destroy_csr(vtk_csr *A) {
     (void)hipFree(A->d_send_idx);
     (void)hipFree(A->d_send_buf);
     (void)hipFree(A->d_lsv);
+    (void)hipFree(A->d_g4tab);
+    (void)hipFree(A->d_g4D);
     free_sell(A);
     (void)hipFree(A->g_in.d_list);
     (void)hipFree(A->g_bd.d_list);
@@ -882,6 +887,87 @@ int line_len_candidate(vtk_csr *A, int64_t &L) {
     return VTK_OK;
 }
 
+// 4D grid structure (vtk::Grid4): tables built and every entry checked on the device; rank-local
+// (the kernels read the tables or the SELL copy, the same bits either way: no agreement needed).
+// VTK_ERR_ARG when the operator is not such a grid (the state is then unchanged).
+int grid4_set(vtk_csr *A, int64_t Ny, int64_t Nvx, int64_t Nvy) {
+    vtk_ctx *c = A->ctx;
+    const int64_t n = A->n_local, S4 = Ny * Nvx * Nvy;
+    if (Ny < 3 || Nvx < 2 || Nvy < 2 || S4 <= 0 || S4 > INT32_MAX || n <= 0 || n % S4 != 0 || A->n_global % S4 != 0 ||
+        n + 2 * S4 >= INT32_MAX / 2)
+        return VTK_ERR_ARG;
+    Grid4 g;
+    g.Ny = (int)Ny;
+    g.Nvx = (int)Nvx;
+    g.Nvy = (int)Nvy;
+    g.X = (int)(n / S4);
+    if (c->dist) {   // across ranks: whole x planes, the halo = the two neighbour planes
+        bool solo = true;
+        BandLayout lay;
+        if (band_check_dist(A, S4, solo, lay) != VTK_OK) return VTK_ERR_ARG;
+        if (!solo) g.lblk = lay.lblk;
+    }
+    if (g.lblk < 0 && g.X < 3) return VTK_ERR_ARG;
+    DBuf tab, D, bad;
+    TRY(dalloc(c, tab, grid4_tab_len(g) * sizeof(double)));
+    TRY(dalloc(c, D, (size_t)n * (A->fp32 ? 4 : 8)));
+    TRY(dalloc(c, bad, sizeof(int)));
+    HIPCHK(c, hipMemsetAsync(tab.p, 0, grid4_tab_len(g) * sizeof(double), c->stream));
+    HIPCHK(c, hipMemsetAsync(bad.p, 0, sizeof(int), c->stream));
+    HIPCHK(c, launch_grid4_build(A->d_indptr, A->d_indices, A->d_data, A->fp32, n, g, tab.as<double>(), D.p,
+                                 bad.as<int>(), c->stream));
+    int hb = 1;
+    HIPCHK(c, hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (hb != 0) return VTK_ERR_ARG;
+    (void)hipFree(A->d_g4tab);
+    (void)hipFree(A->d_g4D);
+    A->d_g4tab = tab.as<double>();
+    A->d_g4D = D.p;
+    tab.p = D.p = nullptr;
+    g.tab = A->d_g4tab;
+    g.D = A->d_g4D;
+    A->g4 = g;
+    return VTK_OK;
+}
+
+// the drop-in path's 4D grid detection: the distinct column distances of the first local row
+// (periodic in n) are 1, Nvy, Nvx Nvy, Ny Nvx Nvy for the 4D Vlasov operators (0: no candidate)
+int grid4_candidate(vtk_csr *A, int64_t &Ny, int64_t &Nvx, int64_t &Nvy) {
+    vtk_ctx *c = A->ctx;
+    const int64_t n = A->n_local, N = A->n_global;
+    Ny = Nvx = Nvy = 0;
+    if (n < 1) return VTK_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int32_t k0 = A->h_indptr[0], k1 = A->h_indptr[1];
+    if (k1 - k0 < 5 || k1 - k0 > 64) return VTK_OK;
+    std::vector<int32_t> idx((size_t)(k1 - k0));
+    HIPCHK(c, hipMemcpy(idx.data(), A->d_indices + k0, (k1 - k0) * sizeof(int32_t), hipMemcpyDeviceToHost));
+    std::vector<int64_t> d;
+    for (int32_t l : idx) {
+        const int64_t g = l < n ? l + A->row_begin : A->halo_cols[(size_t)(l - n)];
+        int64_t dist = std::llabs(g - A->row_begin);
+        dist = std::min(dist, N - dist);
+        if (dist > 0) d.push_back(dist);
+    }
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    if (d.size() != 4 || d[0] != 1 || d[2] % d[1] != 0 || d[3] % d[2] != 0) return VTK_OK;
+    Nvy = d[1];
+    Nvx = d[2] / d[1];
+    Ny = d[3] / d[2];
+    return VTK_OK;
+}
+
+int auto_grid4(vtk_csr *A) {
+    if (!A->ctx->tune.auto_band) return VTK_OK;
+    int64_t Ny, Nvx, Nvy;
+    TRY(grid4_candidate(A, Ny, Nvx, Nvy));
+    if (Ny <= 0) return VTK_OK;
+    const int rc = grid4_set(A, Ny, Nvx, Nvy);
+    return rc == VTK_ERR_ARG ? VTK_OK : rc;
+}
+
 // the drop-in path's line-band detection: the same check vtk_csr_set_line_band runs, on the
 // candidate line length (tuning auto_band 0: off)
 int auto_line_band(vtk_csr *A) {
@@ -981,7 +1067,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // ... except for rows wider than 8 (the 4D operator: 9 entries) without a halo to overlap:
     // there the SpMV + BJ kernel and the streaming dots kernel beat the register-capped fused
     // kernel (C4: 707 + 658 us vs 1473 us per step, 422 vs 405 it/s)
-    const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M);
+    // (with the 4D grid rows (Grid4) the fused kernel loads no values or codes: tuning c4_fused)
+    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused;
+    const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M) && !g4_fused;
     const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9;
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
     const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
@@ -1627,6 +1715,7 @@ int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t
     auto *A = new vtk_csr();
     struct Guard { vtk_csr *&a; ~Guard() { if (a) destroy_csr(a); } } g{A};
     A->ctx = c;
+    A->device = c->device;
     A->n_global = n_global;
     A->offsets = offs;
     A->row_begin = offs[c->rank];
@@ -1670,8 +1759,9 @@ int vtk_csr_create(vtk_ctx *c, int64_t n_global, const int64_t *offsets, int64_t
             return fail(c, VTK_ERR_ARG, "vtk_csr_create: column index out of range");
     }
     TRY(finish_csr(A));
-    // the drop-in path gets the fast solver too: the 2D Vlasov structure is found in the CSR
+    // the drop-in path gets the fast solver too: the 2D / 4D Vlasov structure is found in the CSR
     TRY(auto_line_band(A));
+    if (A->band_L == 0) TRY(auto_grid4(A));
     *out = A;
     A = nullptr;
     return VTK_OK;
@@ -1688,6 +1778,7 @@ int vtk_csr_create_vlasov(vtk_ctx *c, const vtk_vlasov_params *p, const int64_t 
     auto *A = new vtk_csr();
     struct Guard { vtk_csr *&a; ~Guard() { if (a) destroy_csr(a); } } g{A};
     A->ctx = c;
+    A->device = c->device;
     A->n_global = N;
     A->offsets = offs;
     A->row_begin = offs[c->rank];
@@ -1718,6 +1809,11 @@ int vtk_csr_create_vlasov(vtk_ctx *c, const vtk_vlasov_params *p, const int64_t 
         const int brc = band_check_all(A, p->shape[1]);
         if (brc == VTK_OK) A->band_L = p->shape[1];
         else if (brc != VTK_ERR_ARG) return brc;
+    }
+    // the 4D operator's rows are grid rows (couplings by one coordinate each)
+    if (p->dim == 4) {
+        const int grc = grid4_set(A, p->shape[1], p->shape[2], p->shape[3]);
+        if (grc != VTK_OK && grc != VTK_ERR_ARG) return grc;
     }
     *out = A;
     A = nullptr;
@@ -1804,6 +1900,7 @@ int vtk_bjacobi_create_ex(vtk_csr *A, int bs, int setup, vtk_prec **out) {
     auto *M = new vtk_prec();
     struct Guard { vtk_prec *&m; ~Guard() { if (m) vtk_prec_destroy(m); } } g{M};
     M->A = A;
+    M->device = c->device;
     M->bs = bs;
     M->nb = (A->n_local + bs - 1) / bs;
     HIPCHK(c, hipMalloc(&M->d_inv, std::max<int64_t>(M->nb, 1) * bs * bs * sizeof(double)));
@@ -1871,6 +1968,7 @@ int vtk_linejacobi_create(vtk_csr *A, int64_t stride, int64_t seg, vtk_prec **ou
     auto *M = new vtk_prec();
     struct Guard { vtk_prec *&m; ~Guard() { if (m) vtk_prec_destroy(m); } } g{M};
     M->A = A;
+    M->device = c->device;
     M->kind = VTK_PREC_LINE;
     M->bs = 0;
     M->line = line_plan(A->n_local, A->row_begin, stride, seg);
@@ -2035,7 +2133,7 @@ int vtk_bjacobi_get_mode(vtk_prec *M, int *mode_in_use, int *tridiag_available) 
 
 void vtk_prec_destroy(vtk_prec *M) {
     if (!M) return;
-    if (M->A && M->A->ctx) (void)hipSetDevice(M->A->ctx->device);
+    (void)hipSetDevice(M->device);
     (void)hipFree(M->d_inv);
     (void)hipFree(M->d_tri);
     (void)hipFree(M->line.f);
@@ -2067,6 +2165,34 @@ int vtk_csr_set_line_band(vtk_csr *A, int64_t line_len) {
 int vtk_csr_get_line_band(vtk_csr *A, int64_t *line_len) {
     if (!A || !line_len) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_csr_get_line_band: NULL argument");
     *line_len = A->band_L;
+    return VTK_OK;
+}
+
+int vtk_csr_set_grid4(vtk_csr *A, int64_t Ny, int64_t Nvx, int64_t Nvy) {
+    if (!A) return fail(nullptr, VTK_ERR_ARG, "vtk_csr_set_grid4: A is NULL");
+    vtk_ctx *c = A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (Ny == 0) {   // clear
+        (void)hipFree(A->d_g4tab);
+        (void)hipFree(A->d_g4D);
+        A->d_g4tab = nullptr;
+        A->d_g4D = nullptr;
+        A->g4 = Grid4{};
+        return VTK_OK;
+    }
+    const int rc = grid4_set(A, Ny, Nvx, Nvy);
+    if (rc == VTK_ERR_ARG)
+        return fail(c, VTK_ERR_ARG, "vtk_csr_set_grid4: not a 4D grid operator of these extents (rows = whole x planes "
+                                    "of Ny*Nvx*Nvy rows, Ny >= 3, Nvx, Nvy >= 2, each row coupled to x+-1, y+-1, "
+                                    "vx+-1, vy+-1 in ascending column order with values by one coordinate each)");
+    return rc;
+}
+
+int vtk_csr_get_grid4(vtk_csr *A, int64_t *dims) {
+    if (!A || !dims) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_csr_get_grid4: NULL argument");
+    dims[0] = A->d_g4tab ? A->g4.Ny : 0;
+    dims[1] = A->d_g4tab ? A->g4.Nvx : 0;
+    dims[2] = A->d_g4tab ? A->g4.Nvy : 0;
     return VTK_OK;
 }
 

@@ -640,6 +640,66 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
     return hipSuccess;
 }
 
+// 4D grid rows (vtk::Grid4): pass 0 writes every entry's value into its table slot (D[r] for
+// the diagonal), pass 1 compares every entry with its slot bit for bit; either pass flags a row
+// whose stored columns are not the grid kinds in ascending order.  Rows writing different values
+// into one slot leave one of them there, so pass 1 catches every disagreement.
+template <typename VT>
+__global__ __launch_bounds__(NT) void k_grid4_build(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
+                                                    const VT *__restrict__ data, int64_t n, Grid4 g,
+                                                    double *__restrict__ tab, VT *__restrict__ D, int *bad, int pass) {
+    for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
+        const G4Row q = g4_coords(r, g);
+        int64_t c[9];
+        bool p[9];
+        g4_cols(r, q, g, n, c, p);
+        int ord[9], m = 0;
+        for (int k = 0; k < 9; ++k)
+            if (p[k]) ord[m++] = k;
+        for (int i = 1; i < m; ++i)   // ascending columns (the stored order of a canonical CSR)
+            for (int t = i; t > 0 && c[ord[t]] < c[ord[t - 1]]; --t) {
+                const int s = ord[t];
+                ord[t] = ord[t - 1];
+                ord[t - 1] = s;
+            }
+        const int k0 = indptr[r];
+        bool ok = indptr[r + 1] - k0 == m;
+        for (int e = 0; e < m && ok; ++e) {
+            const int kind = ord[e];
+            if ((int64_t)indices[k0 + e] != c[kind] || (e > 0 && c[ord[e]] == c[ord[e - 1]])) { ok = false; break; }
+            const VT dv = data[k0 + e];
+            if (kind == 4) {
+                if (pass == 0) D[r] = dv;
+            } else {
+                const int sl = g4_slot(kind, q, g);
+                if (pass == 0) tab[sl] = (double)dv;
+                else if (__double_as_longlong(tab[sl]) != __double_as_longlong((double)dv)) ok = false;
+            }
+        }
+        if (!ok) atomicOr(bad, 1);
+    }
+}
+
+hipError_t launch_grid4_build(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
+                              const Grid4 &g, double *tab, void *D, int *bad, hipStream_t s) {
+    const int64_t S4 = (int64_t)g.Ny * g.Nvx * g.Nvy;
+    if (g.Ny < 3 || g.Nvx < 2 || g.Nvy < 2 || S4 <= 0 || n % S4 != 0 || n / S4 != g.X || n > INT32_MAX / 2 ||
+        (g.lblk < 0 && g.X < 3))
+        return hipErrorInvalidValue;
+    int64_t gr = (n + NT - 1) / NT;
+    if (gr > 4096) gr = 4096;
+    if (gr < 1) gr = 1;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (fp32) hipLaunchKernelGGL(k_grid4_build<float>, dim3((unsigned)gr), dim3(NT), 0, s, indptr, indices,
+                                     (const float *)data, n, g, tab, (float *)D, bad, pass);
+        else hipLaunchKernelGGL(k_grid4_build<double>, dim3((unsigned)gr), dim3(NT), 0, s, indptr, indices,
+                                (const double *)data, n, g, tab, (double *)D, bad, pass);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 // y = A x from the line-separable tables and the SELL codes (one wave per 64-row chunk, lane per
 // row): k_sell's plain SpMV -- entries in stored order, padding skipped -- reading 12 B of
 // matrix per row instead of 44.  lblk < 0: one rank (x couplings periodic); else the halo

@@ -67,6 +67,63 @@ __device__ __forceinline__ void canon_row(const double *__restrict__ lsv, int n,
     }
 }
 
+// ---- 4D grid rows (vtk::Grid4) -------------------------------------------------------------
+// kinds in the order of a row without periodic wraps: 0 x-1, 1 y-1, 2 vx-1, 3 vy-1, 4 diagonal,
+// 5 vy+1, 6 vx+1, 7 y+1, 8 x+1.  Table slot of kind k's value: tab[g4_slot(k, coordinates)]
+struct G4Row {
+    int ix, iy, jvx, jvy;
+};
+__device__ __forceinline__ G4Row g4_coords(int64_t r, const Grid4 &g) {
+    G4Row q;
+    q.jvy = (int)(r % g.Nvy);
+    int64_t t = r / g.Nvy;
+    q.jvx = (int)(t % g.Nvx);
+    t /= g.Nvx;
+    q.iy = (int)(t % g.Ny);
+    q.ix = (int)(t / g.Ny);
+    return q;
+}
+__device__ __forceinline__ int g4_slot(int kind, const G4Row &q, const Grid4 &g) {
+    const int oy = 2 * g.Nvx, ovx = oy + 2 * g.Nvy, ovy = ovx + 2 * g.X;
+    switch (kind) {
+        case 0: return q.jvx;
+        case 8: return g.Nvx + q.jvx;
+        case 1: return oy + q.jvy;
+        case 7: return oy + g.Nvy + q.jvy;
+        case 2: return ovx + q.ix;
+        case 6: return ovx + g.X + q.ix;
+        case 3: return ovy + q.iy;
+        default: return ovy + g.Ny + q.iy;   // 5
+    }
+}
+// the nine kinds' columns of local row r (n local rows) and whether the row has them (vx, vy
+// Dirichlet); x neighbours periodic inside the slab on one rank (lblk < 0), else halo planes
+__device__ __forceinline__ void g4_cols(int64_t r, const G4Row &q, const Grid4 &g, int64_t n, int64_t (&c)[9],
+                                        bool (&p)[9]) {
+    const int64_t S2 = g.Nvy, S3 = (int64_t)g.Nvx * g.Nvy, S4 = (int64_t)g.Ny * S3;
+    const int64_t rest = r - (int64_t)q.ix * S4;
+    if (g.lblk < 0) {
+        c[0] = (int64_t)(q.ix == 0 ? g.X - 1 : q.ix - 1) * S4 + rest;
+        c[8] = (int64_t)(q.ix == g.X - 1 ? 0 : q.ix + 1) * S4 + rest;
+    } else {
+        c[0] = q.ix >= 1 ? r - S4 : n + (int64_t)g.lblk * S4 + rest;
+        c[8] = q.ix <= g.X - 2 ? r + S4 : n + (int64_t)(1 - g.lblk) * S4 + rest;
+    }
+    c[1] = q.iy == 0 ? r + (int64_t)(g.Ny - 1) * S3 : r - S3;
+    c[7] = q.iy == g.Ny - 1 ? r - (int64_t)(g.Ny - 1) * S3 : r + S3;
+    c[2] = r - S2;
+    c[6] = r + S2;
+    c[3] = r - 1;
+    c[5] = r + 1;
+    c[4] = r;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) p[k] = true;
+    p[2] = q.jvx > 0;
+    p[6] = q.jvx < g.Nvx - 1;
+    p[3] = q.jvy > 0;
+    p[5] = q.jvy < g.Nvy - 1;
+}
+
 // Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
 // 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
 // contiguous id range; with the grid-stride tile loop an XCD then works on a contiguous window

@@ -116,6 +116,22 @@ struct LineOp {
     int compact = 0;
 };
 
+// 4D phase-space grid of the Vlasov operators (row = ((ix Ny + iy) Nvx + jvx) Nvy + jvy, x and y
+// periodic, vx and vy Dirichlet): every row couples to x +- 1 (value by jvx),
+// y +- 1 (by jvy), vx +- 1 (by ix), vy +- 1 (by iy) and itself, in ascending column order.  When
+// vtk_csr_set_grid4 / the Vlasov assembly / the drop-in detection verified that (bit for bit),
+// the solver's SELL launches take each row's columns from its coordinates and its values from
+// D[n] (the stored value type) and the per-coordinate tables: 4 B of matrix per row (C4) instead
+// of 9 values and 9 codes.  X = local x planes; lblk: across ranks the halo block holding the
+// left x neighbour plane (-1: one rank, x periodic inside the slab).
+struct Grid4 {
+    int Ny = 0, Nvx = 0, Nvy = 0, X = 0;
+    int lblk = -1;
+    const double *tab = nullptr;   // TX[2][Nvx] | TY[2][Nvy] | TVX[2][X] | TVY[2][Ny] (-, + each)
+    const void *D = nullptr;       // diagonal per row, the operator's value type
+};
+inline size_t grid4_tab_len(const Grid4 &g) { return 2 * ((size_t)g.Nvx + g.Nvy + g.X + g.Ny); }
+
 // Tuning switches of a context (vtk_ctx_set_tuning): the defaults are the
 // production path, the others exist for in-process A/B measurements and the bit-identity tests
 // (the same sums with and without a byte-saving form).  Initialised from VTK_<KEY> (upper case)
@@ -138,6 +154,8 @@ struct Tuning {
     int debug_band = 0;       // band-check trace on stderr
     int comm_solo = 0;        // vtk_comm_init with world 1 builds a one-rank RCCL communicator
     int auto_band = 1;        // vtk_csr_create detects the line band (drop-in path)
+    int grid4 = 1;            // solver launches read 4D grid rows from their coordinates (Grid4)
+    int c4_fused = 0;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
 };
 }  // namespace vtk
 
@@ -176,6 +194,7 @@ struct vtk_ctx {
 
 struct vtk_csr {
     vtk_ctx *ctx = nullptr;
+    int device = 0;   // the context's device: destroy never dereferences ctx (it may be gone)
     int64_t n_global = 0, row_begin = 0, row_end = 0, n_local = 0, nnz = 0;
     int fp32 = 0;
     int32_t *d_indptr = nullptr, *d_indices = nullptr;  // local column indices
@@ -207,6 +226,10 @@ struct vtk_csr {
     // d_lsv = D | TX | TV; null: not separable (the band step reads the SELL values)
     double *d_lsv = nullptr;
     bool lsv_canon = false;   // ... and every row canonical (canon_order): the band step reads no codes
+    // 4D grid structure (vtk::Grid4; tables owned here); g4_dims = 0: not set
+    vtk::Grid4 g4;
+    double *d_g4tab = nullptr;
+    void *d_g4D = nullptr;
     // distributed band step: the halo is two neighbour lines; peers and the alltoallv layout of
     // the per-step ghost exchange (BAND_GHOST_VECS L doubles per side), -1 offsets: no such side
     bool band_ghost = false;                            // band across ranks: per-step ghost exchange
@@ -219,6 +242,7 @@ struct vtk_csr {
 
 struct vtk_prec {
     vtk_csr *A = nullptr;
+    int device = 0;   // destroy never dereferences A (a finaliser may have freed it first)
     int bs = 8;
     int64_t nb = 0;
     double *d_inv = nullptr;     // [nb][bs][bs]
@@ -256,6 +280,7 @@ struct SpmvIn {
     int lsv_L = 0, lsv_lblk = -1;
     int lsv_canon = 0;   // ... and every row canonical: k_sell computes the columns (canon_row)
     int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX; vtk::Tuning)
+    Grid4 g4{};          // 4D grid rows (solver launches; g4.tab null: not used)
     int swz = 0;         // XCD-aware SELL group order (vtk::Tuning::sell_swz)
 };
 
@@ -446,6 +471,11 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
                            hipStream_t s, int canon, int grid_cap);   // canon: rows canonical, no codes read
+// 4D grid tables (vtk::Grid4) from the CSR (pass 0) and the check (pass 1): *bad |= 1 when an entry
+// is no grid coupling or differs from its table value, |= 2 when a row is not in ascending
+// canonical order; D and tab written here
+hipError_t launch_grid4_build(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
+                              const Grid4 &g, double *tab, void *D, int *bad, hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 

@@ -66,6 +66,7 @@ struct SpmvK {
     int lsv_L, lsv_lblk;
     int canon;   // with lsv: every row canonical (vtk_csr::lsv_canon): columns from canon_row
     int swz;     // XCD-aware group order (xcd_swizzle; vtk::Tuning::sell_swz)
+    Grid4 g4;    // 4D grid rows: columns from the coordinates, values from D / tables (g4.tab null: off)
 };
 
 // value of entry (row, c) from the line-separable tables; drow = D[row], (xl, v) the row's line
@@ -580,6 +581,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // (not in the plain SpMV: vtk_spmv, the measured standalone SpMV, never has lsv, and the
         // extra path cost its loop 249 -> 372 us on C3 through code shape alone)
         constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE && EPI != EPI_PLAIN;
+        constexpr bool G4_OK = (WU == 0 || WU == 9) && !PIPE && EPI != EPI_PLAIN;
         if (CANON_OK && a.canon) {
             if (64 * q < a.n_local) {
                 const int L = a.lsv_L;
@@ -600,6 +602,78 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     }
                 }
                 batch(c, d, [] {});
+            }
+        } else if (G4_OK && a.g4.tab != nullptr) {
+            // 4D grid rows (vtk::Grid4, checked bit for bit at setup): the nine couplings' columns
+            // from the row's coordinates, their values from D and the per-coordinate tables, summed
+            // in the stored (ascending column) order -- the SELL sum, without codes or values
+            if (64 * q < a.n_local) {
+                const Grid4 &g = a.g4;
+                // coordinates: the chunk's first row by divisions (wave-uniform), then the lane
+                const int r0 = 64 * q;
+                int jvy = r0 % g.Nvy, t4 = r0 / g.Nvy;
+                int jvx = t4 % g.Nvx;
+                t4 /= g.Nvx;
+                int iy = t4 % g.Ny, ix = t4 / g.Ny;
+                jvy += lane;
+                while (jvy >= g.Nvy) {
+                    jvy -= g.Nvy;
+                    if (++jvx == g.Nvx) {
+                        jvx = 0;
+                        if (++iy == g.Ny) {
+                            iy = 0;
+                            ++ix;
+                        }
+                    }
+                }
+                if (!act) ix = iy = jvx = jvy = 0;
+                const G4Row qq{ix, iy, jvx, jvy};
+                int64_t c9[9];
+                bool p9[9];
+                g4_cols(row, qq, g, a.n_local, c9, p9);
+                const double *tb = g.tab;
+                const int oy = 2 * g.Nvx, ovx = oy + 2 * g.Nvy, ovy = ovx + 2 * g.X;
+                double d9[9];
+                d9[0] = tb[jvx];
+                d9[8] = tb[g.Nvx + jvx];
+                d9[1] = tb[oy + jvy];
+                d9[7] = tb[oy + g.Nvy + jvy];
+                d9[2] = tb[ovx + ix];
+                d9[6] = tb[ovx + g.X + ix];
+                d9[3] = tb[ovy + iy];
+                d9[5] = tb[ovy + g.Ny + iy];
+                d9[4] = act ? (double)__builtin_nontemporal_load(static_cast<const VT *>(g.D) + row) : 0.0;
+                double xv[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) xv[k] = xload(a, act && p9[k] ? (int)c9[k] : (act ? row : 0));
+                double tk[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) tk[k] = d9[k] * xv[k];
+                // two couplings of one direction on the same side of the row: in column order
+                auto add2 = [&](bool pa, int64_t ca, double ta, bool pb, int64_t cb, double tb2) {
+                    const bool sw = pa && pb && cb < ca;
+                    const double t1 = sw ? tb2 : ta, t2 = sw ? ta : tb2;
+                    const bool p1 = sw ? pb : pa, p2 = sw ? pa : pb;
+                    s = p1 ? s + t1 : s;
+                    s = p2 ? s + t2 : s;
+                };
+                if (act) {
+                    // x planes before the row's plane, then y lines before its line (periodic
+                    // wraps), the in-line block, the y lines and x planes after
+                    add2(c9[0] < row, c9[0], tk[0], c9[8] < row, c9[8], tk[8]);
+                    add2(c9[1] < row, c9[1], tk[1], c9[7] < row, c9[7], tk[7]);
+                    s = p9[2] ? s + tk[2] : s;
+                    s = p9[3] ? s + tk[3] : s;
+                    s = s + tk[4];
+                    s = p9[5] ? s + tk[5] : s;
+                    s = p9[6] ? s + tk[6] : s;
+                    add2(c9[1] > row, c9[1], tk[1], c9[7] > row, c9[7], tk[7]);
+                    add2(c9[0] > row, c9[0], tk[0], c9[8] > row, c9[8], tk[8]);
+                    if constexpr (TRIM) {
+                        if (p9[3] && ii > 0) sub = sub + d9[3];
+                        if (p9[5] && ii < BS - 1) sup = sup + d9[5];
+                    }
+                }
             }
         } else if constexpr (WU > 0) {
             if (64 * q < a.n_local) {
@@ -1042,7 +1116,8 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
                       sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0,
                       sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk,
-                      sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0, in.swz};
+                      sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0, in.swz,
+                      sell ? in.g4 : Grid4{}};
     return a;
 }
 

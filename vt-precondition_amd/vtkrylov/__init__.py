@@ -269,6 +269,18 @@ class CsrOperator:
         check(lib().vtk_csr_get_line_values(self._h, C.byref(v)), self.ctx.handle)
         return v.value
 
+    def set_grid4(self, Ny: int, Nvx: int, Nvy: int):
+        """Declare the 4D phase-space grid structure (vtk_csr_set_grid4; checked on the device, Ny 0
+        clears it).  The 4D Vlasov operators get it automatically, also when uploaded as a CSR."""
+        check(lib().vtk_csr_set_grid4(self._h, int(Ny), int(Nvx), int(Nvy)), self.ctx.handle)
+
+    @property
+    def grid4(self) -> tuple:
+        """(Ny, Nvx, Nvy) of the verified 4D grid structure, (0, 0, 0) when not set."""
+        v = (C.c_int64 * 3)()
+        check(lib().vtk_csr_get_grid4(self._h, v), self.ctx.handle)
+        return tuple(int(t) for t in v)
+
     def layout_info(self) -> dict:
         """Layout in use, bytes of the operator one SpMV reads in it, SELL chunk counts."""
         li = _abi.LayoutInfo()

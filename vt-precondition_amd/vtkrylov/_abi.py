@@ -93,6 +93,8 @@ PROTOTYPES = {
     "vtk_csr_set_line_band": (C.c_int, [P, C.c_int64]),
     "vtk_csr_get_line_band": (C.c_int, [P, I64P]),
     "vtk_csr_get_line_values": (C.c_int, [P, C.POINTER(C.c_int)]),
+    "vtk_csr_set_grid4": (C.c_int, [P, C.c_int64, C.c_int64, C.c_int64]),
+    "vtk_csr_get_grid4": (C.c_int, [P, I64P]),
     "vtk_bjacobi_get_mode": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_destroy": (None, [P]),
     "vtk_linejacobi_create": (C.c_int, [P, C.c_int64, C.c_int64, C.POINTER(P)]),
