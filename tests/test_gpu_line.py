@@ -319,5 +319,10 @@ def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
         x2, i2 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
     assert i2 == 0 and it1 == vk_lib.last_stats().inner_iters
     assert np.array_equal(x1, x2)
+    for wgs in (64, 2048):   # x staged through LDS (k_lsv_ring): the same products, the same order
+        with gpu.tuning(lsv_ring=wgs):
+            x3, i3 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
+        assert i3 == 0 and it1 == vk_lib.last_stats().inner_iters
+        assert np.array_equal(x1, x3), wgs
     M.close()
     A.close()

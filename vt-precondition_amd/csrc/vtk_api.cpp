@@ -80,7 +80,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
     {"band_canon", &Tuning::band_canon}, {"band_canon_sl", &Tuning::band_canon_sl},
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
-    {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
+    {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused},
 };
@@ -952,10 +952,13 @@ int grid4_candidate(vtk_csr *A, int64_t &Ny, int64_t &Nvx, int64_t &Nvy) {
     }
     std::sort(d.begin(), d.end());
     d.erase(std::unique(d.begin(), d.end()), d.end());
-    if (d.size() != 4 || d[0] != 1 || d[2] % d[1] != 0 || d[3] % d[2] != 0) return VTK_OK;
-    Nvy = d[1];
-    Nvx = d[2] / d[1];
-    Ny = d[3] / d[2];
+    // {1, S2, S3, S4}, plus the periodic y wrap S4 - S3 (= (Ny - 1) S3) when Ny > 2
+    if (d.size() < 4 || d.size() > 5 || d[0] != 1) return VTK_OK;
+    const int64_t S2 = d[1], S3 = d[2], S4 = d.back();
+    if (S3 % S2 != 0 || S4 % S3 != 0 || (d.size() == 5 && d[3] != S4 - S3)) return VTK_OK;
+    Nvy = S2;
+    Nvx = S3 / S2;
+    Ny = S4 / S3;
     return VTK_OK;
 }
 
@@ -1176,7 +1179,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
                                           s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
-                                          c->stream, line_canon ? 1 : 0, c->tune.lsv_spmv_cap));
+                                          c->stream, line_canon ? 1 : 0, c->tune.lsv_spmv_cap, c->tune.lsv_ring));
             } else {
                 Prof pf(c, "spmv", j, b_csr + 2 * n8);
                 HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,

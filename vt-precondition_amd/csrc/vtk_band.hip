@@ -766,10 +766,88 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
     }
 }
 
+// The same SpMV with the x vector staged through LDS (one rank, canonical rows): workgroup (range
+// rb, part h) walks the lines of its range in order, loads each line's x rows v0-8 .. v0+LP+7 once
+// (coalesced, prefetched one line ahead in registers) into a ring of 4 lines, and forms row v of
+// line x from the ring -- x-1 and x+1 at v, x at v-1..v+1 -- with canon_order's straight-line
+// sum (the same products added in the same order as k_lsv_spmv<CANON>: bit-identical).  HBM
+// reads x once (+2 halo lines per range) instead of gathering it three times from L2/MALL.
+__global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ lsv, const double *__restrict__ x,
+                                                     double *__restrict__ y, int n, int L, int H, const int *stop_col,
+                                                     int col) {
+    __shared__ double ring[4 * BAND_T];
+    if (stopped(stop_col, col)) return;
+    const int tid = threadIdx.x, X = n / L, LP = L / H;
+    const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
+    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R), nl = xb - xa;
+    const int v = v0 - 8 + tid;
+    const bool inl = v >= 0 && v < L && tid < LP + 16;   // a row of the line (own or v-halo)
+    const bool own = tid >= 8 && tid < 8 + LP;
+    const double tx0 = own ? lsv[n + v] : 0.0, tx1 = own ? lsv[n + L + v] : 0.0;
+    auto line_of = [&](int it) { return it == 0 ? (xa == 0 ? X - 1 : xa - 1) : (it == nl + 1 ? (xb == X ? 0 : xb) : xa - 1 + it); };
+    auto slot = [&](int it) { return (it & 3) * BAND_T; };
+    // prefetch: x of line_of(it) on the lane's row, D of line it - 1 (computed at iteration it)
+    double nxv = inl ? __builtin_nontemporal_load(x + (int64_t)line_of(0) * L + v) : 0.0, nd = 0.0;
+    for (int it = 0; it <= nl + 1; ++it) {
+        ring[slot(it) + tid] = nxv;
+        const double drow = nd;
+        if (it <= nl) {
+            nxv = inl ? __builtin_nontemporal_load(x + (int64_t)line_of(it + 1) * L + v) : 0.0;
+            nd = own && it + 1 >= 2 ? __builtin_nontemporal_load(lsv + (int64_t)(xa + it - 1) * L + v) : 0.0;
+        }
+        __syncthreads();
+        if (it >= 2) {
+            const int xl = xa + it - 2;   // line x: ring slots it-2 (x-1), it-1 (x), it (x+1)
+            const double tv0 = lsv[n + 2 * L + xl], tv1 = lsv[n + 2 * L + X + xl];
+            int64_t cxm, cxp;
+            const int ord = __builtin_amdgcn_readfirstlane(canon_order_xv(xl, 0, n, L, X, -1, cxm, cxp));
+            constexpr int P_MID = 0 | 1 << 3 | 2 << 6 | 3 << 9 | 4 << 12;
+            constexpr int P_FIRST = 1 | 2 << 3 | 3 << 6 | 4 << 9 | 0 << 12;
+            const int sx = slot(it - 1);
+            const double t0 = tx0 * ring[slot(it - 2) + tid];
+            const double t4 = tx1 * ring[slot(it) + tid];
+            const double t2 = drow * ring[sx + tid];
+            const double t1 = tv0 * ring[sx + tid - (tid > 0 ? 1 : 0)];
+            const double t3 = tv1 * ring[sx + tid + (tid < BAND_T - 1 ? 1 : 0)];
+            const bool h1 = v > 0, h3 = v < L - 1;
+            double sa = 0.0;
+            if (ord == P_MID) {
+                sa = sa + t0;
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+                sa = sa + t4;
+            } else if (ord == P_FIRST) {   // line 0: x-1 wraps to line X-1, last
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+                sa = sa + t4;
+                sa = sa + t0;
+            } else {                        // line X-1: x+1 wraps to line 0, first
+                sa = sa + t4;
+                sa = sa + t0;
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+            }
+            if (own) __builtin_nontemporal_store(sa, y + (int64_t)xl * L + v);
+        }
+    }
+}
+
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s, int canon, int grid_cap) {
+                           hipStream_t s, int canon, int grid_cap, int ring_wgs) {
     if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || (halo && lblk < 0)) return hipErrorInvalidValue;
+    if (ring_wgs > 0 && canon && !halo) {   // the LDS-staged form (one rank, canonical rows)
+        const int H = band_parts(L);
+        const int64_t X = n / L;
+        if (H >= 1 && X >= 3) {
+            const int64_t R = std::max<int64_t>(1, std::min<int64_t>(ring_wgs / H, X / 2));
+            hipLaunchKernelGGL(k_lsv_ring, dim3((unsigned)(R * H)), dim3(BAND_T), 0, s, lsv, x, y, (int)n, L, H, stop_col, col);
+            return hipGetLastError();
+        }
+    }
     const int64_t nch = (n + 63) / 64;
     // grid_cap: 8192 workgroups by default (vtk::Tuning::lsv_spmv_cap; C3 line solve, in-process
     // A/B: 8.69 ms vs 8.73 at 2048 and 8.85 with one chunk per wave; an XCD swizzle of the chunks

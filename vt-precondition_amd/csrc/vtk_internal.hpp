@@ -146,9 +146,12 @@ struct Tuning {
     int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
     int plain_grid = 2048;    // workgroups of the plain SELL SpMV
     int sell_swz = 0;         // SELL launches walk their groups in XCD-contiguous order
-    int band_opt = 0;         // band step variant bits (vtk_band.hip k_band_step OPT)
+    int band_opt = 3;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
+                              // C3: SpMV operands prefetched j00 254 -> 217 us, + three workgroups per
+                              // CU for j <= 2: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms)
     int band_j3 = 2;          // ... bit 1 (three workgroups per CU) for steps j <= band_j3
     int lsv_spmv_cap = 8192;  // workgroups of the line path's table SpMV
+    int lsv_ring = 0;         // > 0: that table SpMV with x staged through LDS, ~that many workgroups
     int ev_every = 1;         // host throttle event every this many Arnoldi steps (1..LOOKAHEAD+1)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
     int debug_band = 0;       // band-check trace on stderr
@@ -470,7 +473,9 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
 // k_sell's plain SpMV, the same bits.  halo != null: the distributed layout (lblk the left block)
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s, int canon, int grid_cap);   // canon: rows canonical, no codes read
+                           hipStream_t s, int canon, int grid_cap,
+                           int ring_wgs = 0);   // canon: rows canonical, no codes read; ring_wgs > 0: LDS-staged x
+                                                // (k_lsv_ring, about that many workgroups; one rank, canon)
 // 4D grid tables (vtk::Grid4) from the CSR (pass 0) and the check (pass 1): *bad |= 1 when an entry
 // is no grid coupling or differs from its table value, |= 2 when a row is not in ascending
 // canonical order; D and tab written here
