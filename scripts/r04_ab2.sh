@@ -13,5 +13,6 @@ for rep in 1 2; do
   done
 done
 run line_ring 300 python tools/ab_env.py --env lsv_ring --values 0,1024,2048,4096 --rounds 6 --prec line
+run line_sweep 300 python tools/ab_env.py --env line_sweep --values 0,512,1024,2048 --rounds 6 --prec line --perj
 run c4_g4 600 python tools/ab_env.py --config C4 --env grid4 --values 1,0 --rounds 3
 run c4_fused 600 python tools/ab_env.py --config C4 --env c4_fused --values 0,1 --rounds 3

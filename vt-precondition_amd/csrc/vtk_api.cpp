@@ -80,7 +80,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
     {"band_canon", &Tuning::band_canon}, {"band_canon_sl", &Tuning::band_canon_sl},
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
-    {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
+    {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused},
 };
@@ -1015,6 +1015,12 @@ struct Solver {
     }
     double *w3 = nullptr;
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
+    // line path with the fused update + table SpMV (k_line_sweep): p_j in pbuf[j & 1] (V[0] at
+    // j = 0), never in V[j]; sweep_R line ranges
+    bool sweep = false;
+    int sweep_R = 0;
+    double *pbuf[2] = {nullptr, nullptr};
+    const double *p_of(int j) const { return sweep && j > 0 ? pbuf[j & 1] : V + (size_t)j * ld; }
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
@@ -1172,9 +1178,11 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             cnt = spmv_grid(in);
         } else if (line_dc) {
-            // line path: SpMV, then the line sweeps with the step's dots fused behind them
+            // line path: SpMV, then the line sweeps with the step's dots fused behind them (with
+            // the fused update + SpMV sweep, tmp = A p_j already came from step j-1's sweep)
             TRY(halo_exchange(s.A, pj));
-            if (line_lsv) {
+            if (s.sweep && j > 0) {
+            } else if (line_lsv) {
                 // line-separable values: 12 B of matrix per row (codes + diagonal)
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
@@ -1186,7 +1194,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                       nullptr, stop, j, c->stream));
             }
             { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
-              HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream)); }
+              HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, s.p_of(j), s.dcpart, s.G, stop, j, c->stream)); }
             cnt = s.G;
         } else {
             Red h0, d0;
@@ -1251,6 +1259,29 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.opt = s.ghost ? 0 : c->tune.band_opt;   // variants exist for the one-rank instantiation
             a.j3 = std::min(c->tune.band_j3, BAND_J3);
             HIPCHK(c, launch_band_step(a, s.band_grid(j, a.opt, a.j3), s.A->sell.uniform_w, c->stream));
+        } else if (s.sweep) {
+            // update pass of step j + the table SpMV of p_{j+1} (none after the cycle's last step)
+            const bool sp = j + 1 < m;
+            Prof pf(c, "line_sweep", j, n8 * (j + 4) + (sp ? 2 * n8 : 0.0));   // V_j, p, w; v_j, p_{j+1} (+ D, y)
+            LineSweepK a;
+            a.V = s.V;
+            a.ld = s.ld;
+            a.j = j;
+            a.m = m;
+            a.p_in = s.p_of(j);
+            a.p_out = s.pbuf[(j + 1) & 1];
+            a.w = w_cur;
+            a.cf = s.cf;
+            a.st = ds;
+            a.x = s.x;
+            a.H = s.H;
+            a.S = s.S;
+            a.lsv = s.A->d_lsv;
+            a.y = sp ? s.tmp : nullptr;
+            a.n = (int)n;
+            a.L = (int)s.A->band_L;
+            a.H_parts = band_parts(s.A->band_L);
+            HIPCHK(c, launch_line_sweep(a, s.sweep_R, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
             HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
@@ -1340,7 +1371,21 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const size_t nghost = (s.band && A->band_ghost)
                               ? (size_t)2 * (m + 2) * A->band_L + 4 * (size_t)BAND_GHOST_VECS * A->band_L : 0;
     const size_t nedge = s.band ? (size_t)s.ld + nghost : 0;
-    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge + 16;
+    // line path: the update pass fused with the next table SpMV (k_line_sweep; one rank, the
+    // line-Jacobi dots kernel, canonical line-separable rows, restart <= 20); p apart from V
+    if (dc && !c->dist && c->tune.line_sweep > 0 && M && M->kind == VTK_PREC_LINE && M->line.seg >= 1 &&
+        M->line.seg <= 32 && A->d_lsv && A->band_L > 0 && A->lsv_canon && c->tune.band_lsv && c->tune.sell_canon &&
+        A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && m <= 20) {
+        const int H = band_parts(A->band_L);
+        const int64_t X = n / A->band_L;
+        if (H >= 1 && X >= 3 && n % A->band_L == 0) {
+            s.sweep = true;
+            s.sweep_R = (int)std::max<int64_t>(1, std::min<int64_t>(c->tune.line_sweep / H, X / 2));
+        }
+    }
+    const size_t npb = s.sweep ? 2 * (size_t)s.ld : 0;
+    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge +
+                      npb + 16;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
         c->ws = nullptr;
@@ -1373,6 +1418,11 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             s.grecv = s.gsend + 2 * (size_t)BAND_GHOST_VECS * A->band_L;
         }
         wp += nedge;
+    }
+    if (s.sweep) {
+        s.pbuf[0] = wp;
+        s.pbuf[1] = wp + s.ld;
+        wp += npb;
     }
     HIPCHK(c, hipMemsetAsync(s.H, 0, (size_t)m * (m + 1) * sizeof(double), c->stream));
     HIPCHK(c, hipMemsetAsync(s.giv, 0, (size_t)2 * m * sizeof(double), c->stream));
@@ -1537,9 +1587,10 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
                 // the x update ran in update pass xup_tag: account it as the "xupdate" class and
                 // drop the host-enqueued k_xupdate (it returned at entry)
                 const int cu = prof_class(c, "dc_update"), cb = prof_class(c, "band_step"), cx = prof_class(c, "xupdate");
+                const int cw = prof_class(c, "line_sweep");
                 for (size_t i = 0; i < xup_idx && i < c->prof_pending.size(); ++i) {
                     auto &p = c->prof_pending[i];
-                    if ((p.cls == cu || p.cls == cb) && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
+                    if ((p.cls == cu || p.cls == cb || p.cls == cw) && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
                 }
                 if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].col = BIG_COL;
             }

@@ -835,6 +835,148 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
     }
 }
 
+// the canonical table SpMV of line xl (one rank) from a ring of x lines: slots sm (x-1), sx (x),
+// sp (x+1), lane tid <-> position v; the same products in the same order as k_lsv_spmv<CANON>
+__device__ __forceinline__ double ring_line_spmv(const double *ring, int sm, int sx, int sp, int tid, int v, int L,
+                                                 int X, int n, int xl, double tx0, double tx1, double drow,
+                                                 const double *__restrict__ lsv) {
+    const double tv0 = lsv[n + 2 * L + xl], tv1 = lsv[n + 2 * L + X + xl];
+    int64_t cxm, cxp;
+    const int ord = __builtin_amdgcn_readfirstlane(canon_order_xv(xl, 0, n, L, X, -1, cxm, cxp));
+    constexpr int P_MID = 0 | 1 << 3 | 2 << 6 | 3 << 9 | 4 << 12;
+    constexpr int P_FIRST = 1 | 2 << 3 | 3 << 6 | 4 << 9 | 0 << 12;
+    const double t0 = tx0 * ring[sm + tid];
+    const double t4 = tx1 * ring[sp + tid];
+    const double t2 = drow * ring[sx + tid];
+    const double t1 = tv0 * ring[sx + tid - (tid > 0 ? 1 : 0)];
+    const double t3 = tv1 * ring[sx + tid + (tid < BAND_T - 1 ? 1 : 0)];
+    const bool h1 = v > 0, h3 = v < L - 1;
+    double sa = 0.0;
+    if (ord == P_MID) {
+        sa = sa + t0;
+        sa = h1 ? sa + t1 : sa;
+        sa = sa + t2;
+        sa = h3 ? sa + t3 : sa;
+        sa = sa + t4;
+    } else if (ord == P_FIRST) {   // line 0: x-1 wraps to line X-1, last
+        sa = h1 ? sa + t1 : sa;
+        sa = sa + t2;
+        sa = h3 ? sa + t3 : sa;
+        sa = sa + t4;
+        sa = sa + t0;
+    } else {                        // line X-1: x+1 wraps to line 0, first
+        sa = sa + t4;
+        sa = sa + t0;
+        sa = h1 ? sa + t1 : sa;
+        sa = sa + t2;
+        sa = h3 ? sa + t3 : sa;
+    }
+    return sa;
+}
+
+// Line path: k_dc_update's pass of step j and the table SpMV of p_{j+1} in one walk over the
+// x-lines: the workgroup of (range, part) updates line y (its rows and one v-halo
+// row each side; the x-halo lines before and after the range recomputed, not stored), puts
+// p_{j+1}(y) into an LDS ring of 4 lines, and forms y = A p_{j+1} on line y - 1 from the ring.
+// p_{j+1} is not re-read for the SpMV; one launch instead of two.  The next line's operands are
+// loaded one line ahead.  Same operations as k_dc_update and k_lsv_spmv<CANON>: bit-identical.
+template <int J>
+__global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) void k_line_sweep(LineSweepK a) {
+    constexpr int j = J;
+    __shared__ double ring[4 * BAND_T];
+    __shared__ double cs[BAND_JV + 1], ce[BAND_JV + 1];
+    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
+        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, nullptr,
+                   a.p_in);
+        return;
+    }
+    if (stopped(&a.st->stop_col, j)) return;
+    const int tid = threadIdx.x, n = a.n, L = a.L, X = n / L, LP = L / a.H_parts;
+    const int b = blockIdx.x, R = (int)gridDim.x / a.H_parts, rb = b / a.H_parts, h = b % a.H_parts, v0 = h * LP;
+    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R), nl = xb - xa;
+    const int v = v0 - 8 + tid;
+    const bool inl = v >= 0 && v < L && tid < LP + 16;   // the part's rows and its v-halo rows
+    const bool own = tid >= 8 && tid < 8 + LP;
+    const bool spmv = a.y != nullptr;
+    for (int k = tid; k <= j; k += BAND_T) {
+        if (k < j) cs[k] = a.cf->s[k];
+        ce[k] = a.cf->e[k];
+    }
+    const double rinv = a.cf->rinv, q = a.cf->q;
+    const double tx0 = own ? a.lsv[n + v] : 0.0, tx1 = own ? a.lsv[n + L + v] : 0.0;
+    __syncthreads();
+    const double ej = ce[j];
+    auto line_of = [&](int it) { return it == 0 ? (xa == 0 ? X - 1 : xa - 1) : (it == nl + 1 ? (xb == X ? 0 : xb) : xa - 1 + it); };
+    struct Ld {
+        double v[J > 0 ? J : 1];
+        double p, w, drow;
+    };
+    // every lane loads (rows outside the part clamped to v0, their values unused): no exec-mask
+    // blocks around the loads, so the wait for this line's operands need not wait for the next's
+    const int vc = inl ? v : v0;
+    auto load = [&](int it, Ld &o) {
+        const int64_t row = (int64_t)line_of(it) * L + vc;
+        o.p = __builtin_nontemporal_load(a.p_in + row);
+        o.w = __builtin_nontemporal_load(a.w + row);
+        const double *pv = a.V + row;
+#pragma unroll
+        for (int k = 0; k < J; ++k) {
+            o.v[k] = __builtin_nontemporal_load(pv);
+            pv += a.ld;
+        }
+        const int xs = it >= 2 ? xa + it - 2 : xa;
+        o.drow = __builtin_nontemporal_load(a.lsv + (int64_t)xs * L + vc);
+    };
+    Ld nx;
+    load(0, nx);
+    for (int it = 0; it <= nl + 1; ++it) {
+        const Ld cu = nx;
+        double av = cu.p, t = cu.w;
+#pragma unroll
+        for (int k = 0; k < J; ++k) {
+            const double sk = cs[k], ek = ce[k];
+            av = av - sk * cu.v[k];
+            t = t - ek * cu.v[k];
+        }
+        double vj = cu.p;
+        if (j >= 1) vj = av * rinv;
+        t = t - ej * vj;
+        const double pn = t * q;
+        if (it >= 1 && it <= nl && own) {   // an owned line: store v_j and p_{j+1}
+            const int64_t row = (int64_t)(xa - 1 + it) * L + v;
+            if (j >= 1) __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+            __builtin_nontemporal_store(pn, a.p_out + row);
+        }
+        ring[(it & 3) * BAND_T + tid] = inl ? pn : 0.0;
+        if (it <= nl) load(it + 1, nx);
+        __syncthreads();
+        if (spmv && it >= 2) {
+            const int xl = xa + it - 2;
+            const double s = ring_line_spmv(ring, ((it - 2) & 3) * BAND_T, ((it - 1) & 3) * BAND_T, (it & 3) * BAND_T, tid,
+                                            v, L, X, n, xl, tx0, tx1, cu.drow, a.lsv);
+            if (own) __builtin_nontemporal_store(s, a.y + (int64_t)xl * L + v);
+        }
+    }
+}
+
+hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s) {
+    const int H = a.H_parts;
+    if (H < 1 || a.L % H != 0 || a.L / H > BAND_LP || (a.L / H) % 8 != 0 || a.n % a.L != 0 || a.n / a.L < 3 ||
+        ranges < 1 || ranges > a.n / a.L / 2 || a.j + 1 > BAND_JV + 1)
+        return hipErrorInvalidValue;
+    const dim3 g((unsigned)(ranges * H)), blk(BAND_T);
+    switch (a.j) {
+#define VTK_SWEEP_J(J_) \
+    case J_: hipLaunchKernelGGL((k_line_sweep<J_>), g, blk, 0, s, a); break;
+        VTK_SWEEP_J(0) VTK_SWEEP_J(1) VTK_SWEEP_J(2) VTK_SWEEP_J(3) VTK_SWEEP_J(4) VTK_SWEEP_J(5) VTK_SWEEP_J(6)
+        VTK_SWEEP_J(7) VTK_SWEEP_J(8) VTK_SWEEP_J(9) VTK_SWEEP_J(10) VTK_SWEEP_J(11) VTK_SWEEP_J(12) VTK_SWEEP_J(13)
+        VTK_SWEEP_J(14) VTK_SWEEP_J(15) VTK_SWEEP_J(16) VTK_SWEEP_J(17) VTK_SWEEP_J(18) VTK_SWEEP_J(19)
+#undef VTK_SWEEP_J
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
                            hipStream_t s, int canon, int grid_cap, int ring_wgs) {

@@ -390,7 +390,8 @@ __device__ inline void hess_solve(const double *__restrict__ H, const double *__
 // it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
 static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
                                         const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
-                                        const double *__restrict__ S, int m, const double *__restrict__ wprev) {
+                                        const double *__restrict__ S, int m, const double *__restrict__ wprev,
+                                        const double *__restrict__ pj_at = nullptr) {
     __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ], ep[DC_MAXJ];
     __shared__ double rinv_s, qp_s;
     // wprev (line-band step): p_j is not stored; recompute it as step j-1 formed it
@@ -407,7 +408,8 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
         }
     __syncthreads();
     const double rinv = rinv_s, qp = qp_s;
-    const double *pj = V + (size_t)j * ld;
+    // p_j: V[j] (the update pass stores it there), or pj_at (the line sweep keeps p apart)
+    const double *pj = pj_at ? pj_at : V + (size_t)j * ld;
     const int kv = c == j ? j : c + 1;   // stored basis vectors in the sum
     const int64_t stride = 2 * (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += stride) {

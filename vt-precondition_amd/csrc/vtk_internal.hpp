@@ -152,6 +152,7 @@ struct Tuning {
     int band_j3 = 2;          // ... bit 1 (three workgroups per CU) for steps j <= band_j3
     int lsv_spmv_cap = 8192;  // workgroups of the line path's table SpMV
     int lsv_ring = 0;         // > 0: that table SpMV with x staged through LDS, ~that many workgroups
+    int line_sweep = 0;       // > 0: line path update pass fused with the next table SpMV, ~that many workgroups
     int ev_every = 1;         // host throttle event every this many Arnoldi steps (1..LOOKAHEAD+1)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
     int debug_band = 0;       // band-check trace on stderr
@@ -481,6 +482,27 @@ hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double
 // canonical order; D and tab written here
 hipError_t launch_grid4_build(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
                               const Grid4 &g, double *tab, void *D, int *bad, hipStream_t s);
+// Line-path DCGS2 update pass of step j fused with the next step's table SpMV (k_line_sweep,
+// one rank, canonical line-separable rows): v_j -> V[j], p_{j+1} -> p_out, y = A p_{j+1} (y null:
+// no SpMV, the cycle's last step), the x update when the step stopped the cycle (st->xup_tag == j).
+// p_j is read from p_in (V[0] at j = 0), never from V[j]: the halo lines another workgroup
+// recomputes stay readable while V[j] is overwritten.
+struct LineSweepK {
+    double *V;
+    int64_t ld;
+    int j, m;
+    const double *p_in;
+    double *p_out;
+    const double *w;
+    const DcCoef *cf;
+    const GmresState *st;
+    double *x;
+    const double *H, *S;
+    const double *lsv;
+    double *y;
+    int n, L, H_parts;
+};
+hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 
