@@ -171,11 +171,11 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
     for A in (G, U):
         M = vk_lib.block_jacobi(A, 8)
         for orth in ("dcgs2", "mgs"):
-            x1, i1, s1 = _solve(vk_lib, A, M, b, orth=orth)
-            with gpu.tuning(grid4=0):
+            with gpu.tuning(c4_fused=0):   # the split step (SpMV + BJ, then the dots)
+                x1, i1, s1 = _solve(vk_lib, A, M, b, orth=orth)
+            with gpu.tuning(grid4=0):      # ... reading the SELL values and codes
                 x0, i0, s0 = _solve(vk_lib, A, M, b, orth=orth)
-            with gpu.tuning(c4_fused=1):
-                x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)
+            x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)   # default: grid rows, dots fused
             assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
             assert np.array_equal(x1, x0), "grid rows change the bits"
             if orth == "mgs":
@@ -197,8 +197,8 @@ def test_grid4_rejects_other_structures(vk_lib, gpu):
     p = twin.CONFIGS["S4"]
     ip, ix, d = coracle.generate(p)
     A = vk_lib.csr_matrix(sp.csr_matrix((d, ix, ip), shape=(p.n, p.n)), ctx=gpu)
-    with pytest.raises(ValueError):
-        A.set_grid4(p.shape[1], p.shape[3], p.shape[2])   # swapped velocity extents
+    with pytest.raises(ValueError):   # another split of the plane into (vx, vy)
+        A.set_grid4(p.shape[1], p.shape[2] * 2, p.shape[3] // 2)
     assert A.grid4 == tuple(p.shape[1:])                   # the detected structure is kept
     A.set_grid4(0, 0, 0)
     assert A.grid4 == (0, 0, 0)

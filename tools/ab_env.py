@@ -76,7 +76,9 @@ def main():
             pr = ctx.profile_read()
             ctx.profile(False)
             perj[v] = {k: round(e["avg_us"], 1) for k, e in sorted(pr.items())
-                       if k.startswith("band_step") or k in ("dc_scalar", "dc_update", "spmv_resid_bj", "spmv_bj_dc")}
+                       if k.startswith("band_step") or k in ("dc_scalar", "dc_update", "spmv_resid_bj", "spmv_bj_dc",
+                                                             "line_sweep", "line_dc", "spmv_lsv", "xupdate", "spmv_bj",
+                                                             "dc_dots", "spmv_resid")}
         ctx.set_tuning("prof_perj", 0)
     out = {"config": a.config, "set": a.set, "perj_us": perj, "prec": a.prec, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,
            "median_ms": {v: statistics.median(t) for v, t in times.items()}, "ms": times}

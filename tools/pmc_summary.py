@@ -46,6 +46,8 @@ CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv
     "xupdate": "vtk::k_xupdate(",
     "bj_apply": "vtk::k_bj_apply",
     "scale0": "vtk::k_scale0(",
+    "line_sweep": "void vtk::k_line_sweep<",
+    "spmv_lsv": r"(void )?vtk::k_lsv_(spmv<|ring\()",
 }
 
 

@@ -79,7 +79,7 @@ struct TuneKey { const char *name; int Tuning::*mem; };
 constexpr TuneKey TUNE_KEYS[] = {
     {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
     {"band_canon", &Tuning::band_canon}, {"band_canon_sl", &Tuning::band_canon_sl},
-    {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
+    {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused},
@@ -342,6 +342,7 @@ SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nu
     }
     in.plain_grid = A->ctx->tune.plain_grid;
     in.swz = A->ctx->tune.sell_swz;
+    in.plain_var = A->ctx->tune.plain_var;
     return in;
 }
 
@@ -1077,7 +1078,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // there the SpMV + BJ kernel and the streaming dots kernel beat the register-capped fused
     // kernel (C4: 707 + 658 us vs 1473 us per step, 422 vs 405 it/s)
     // (with the 4D grid rows (Grid4) the fused kernel loads no values or codes: tuning c4_fused)
-    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused;
+    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused;   // C4 A/B: 213.8 -> 210.3 ms
     const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M) && !g4_fused;
     const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9;
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel

@@ -146,6 +146,7 @@ struct Tuning {
     int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
     int plain_grid = 2048;    // workgroups of the plain SELL SpMV
     int sell_swz = 0;         // SELL launches walk their groups in XCD-contiguous order
+    int plain_var = 0;        // plain SELL SpMV variant bits (k_sell VAR: 1 = padding gathers branched)
     int band_opt = 3;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
                               // C3: SpMV operands prefetched j00 254 -> 217 us, + three workgroups per
                               // CU for j <= 2: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms)
@@ -159,7 +160,7 @@ struct Tuning {
     int comm_solo = 0;        // vtk_comm_init with world 1 builds a one-rank RCCL communicator
     int auto_band = 1;        // vtk_csr_create detects the line band (drop-in path)
     int grid4 = 1;            // solver launches read 4D grid rows from their coordinates (Grid4)
-    int c4_fused = 0;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
+    int c4_fused = 1;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
 };
 }  // namespace vtk
 
@@ -286,6 +287,7 @@ struct SpmvIn {
     int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX; vtk::Tuning)
     Grid4 g4{};          // 4D grid rows (solver launches; g4.tab null: not used)
     int swz = 0;         // XCD-aware SELL group order (vtk::Tuning::sell_swz)
+    int plain_var = 0;   // plain SELL SpMV variant bits (vtk::Tuning::plain_var; k_sell VAR)
 };
 
 LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);

@@ -440,7 +440,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // chunk's code words are all issued with its dictionary and the entry loop has compile-time
 // bounds, so a row wider than one code word (C4: 9 entries) costs no extra dependent round trip
 // for its second word and no batch boundary at the word edge.
-template <typename VT, bool HALO, int EPI, int BS, bool TRI = false, int PSWT = 0, int WU = 0>
+// VAR bit 0 (plain SpMV): padding slots branch around their gather instead of gathering the
+// lane's own row (VTK_GATHER_UNCOND, which the 9-wide C4 rows want)
+template <typename VT, bool HALO, int EPI, int BS, bool TRI = false, int PSWT = 0, int WU = 0, int VAR = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE))) void k_sell(SpmvK<VT, HALO> a) {
     // entries per load batch (DC: registers; PSWT: a row length the launch picked; WU without
     // PSWT: the whole row in one batch)
@@ -559,7 +561,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 // entry) instead of branching around the load: the gathers issue back to back
                 // with no exec-mask blocks.  (x[0] for every padding slot measured 1.6x slower on
                 // C4: one hot L2 line for the whole chip.)
-                if constexpr (VTK_GATHER_UNCOND) xv[u] = xload(a, c[u] >= 0 ? c[u] : (act ? row : 0));
+                if constexpr (VTK_GATHER_UNCOND && !(VAR & 1)) xv[u] = xload(a, c[u] >= 0 ? c[u] : (act ? row : 0));
                 else xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
             }
             mid();
@@ -582,6 +584,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // extra path cost its loop 249 -> 372 us on C3 through code shape alone)
         constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE && EPI != EPI_PLAIN;
         constexpr bool G4_OK = (WU == 0 || WU == 9) && !PIPE && EPI != EPI_PLAIN;
+        // the line-separable tables are a solver-launch form: compiled out of the plain SpMV (its
+        // per-entry value selection cost the measured kernel 222 -> 242 us on C3)
+        constexpr bool LSV_OK = EPI != EPI_PLAIN;
         if (CANON_OK && a.canon) {
             if (64 * q < a.n_local) {
                 const int L = a.lsv_L;
@@ -699,7 +704,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     }
                     // the row's values do not depend on the column form: issued with the codes
                     // and the dictionary, before the form test waits for the dictionary
-                    if (!a.lsv) {
+                    if (!(LSV_OK && a.lsv)) {
 #pragma unroll
                         for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
                     }
@@ -707,7 +712,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 // line-separable values: the row's diagonal, line and position
                 double lsv_d = 0.0;
                 int lsv_x = 0, lsv_v = 0;
-                if (a.lsv) {
+                if (LSV_OK && a.lsv) {
                     lsv_x = (64 * q) / a.lsv_L;
                     lsv_v = 64 * q - lsv_x * a.lsv_L + lane;
                     while (lsv_v >= a.lsv_L) {
@@ -740,7 +745,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                                 const int off = __shfl(dv, code, 64);
                                 c[u] = code != PK_CODES ? row + off : -1;
                             }
-                            d[u] = a.lsv ? (c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0) : (double)dall[k];
+                            d[u] = (LSV_OK && a.lsv) ? (c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0) : (double)dall[k];
                         }
                         batch(c, d, [&] {
                             if constexpr (PIPE) {
@@ -777,7 +782,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
             const int32_t *cc = a.sell_col + o0 + lane;
             double lsv_d = 0.0;
             int lsv_x = 0, lsv_v = 0;
-            if (a.lsv) {
+            if (LSV_OK && a.lsv) {
                 lsv_x = (64 * q) / a.lsv_L;
                 lsv_v = 64 * q - lsv_x * a.lsv_L + lane;
                 while (lsv_v >= a.lsv_L) {
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     // values do not wait for the codes: padding slots hold 0 and are skipped
 #pragma unroll
                     for (int u = 0; u < PSW; ++u) {
-                        if (a.lsv) d[u] = c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0;
+                        if (LSV_OK && a.lsv) d[u] = c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0;
                         else d[u] = (VTK_VAL_EARLY ? (h + u < 8 && k0 + h + u < w) : c[u] >= 0)
                                         ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
                     }
@@ -1136,6 +1141,7 @@ static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const doub
         const dim3 gp(sell ? (unsigned)std::max(1, std::min(in.groups->count, plain_grid(in))) : g.x);
         const int wu = sell_wu_plain(in);
         if (sell && wu == 9) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false, 0, 9>), gp, blk, 0, s, a);
+        else if (sell && (in.plain_var & 1)) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false, 0, 0, 1>), gp, blk, 0, s, a);
         else if (sell) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PLAIN, 1, false>), gp, blk, 0, s, a);
         else hipLaunchKernelGGL((k_spmv<VT, HALO, EPI_PLAIN, 1, false>), g, blk, 0, s, a);
         return hipGetLastError();
