@@ -203,7 +203,7 @@ def test_grid4_rejects_other_structures(vk_lib, gpu):
     A.set_grid4(0, 0, 0)
     assert A.grid4 == (0, 0, 0)
     d2 = d.copy()
-    d2[ip[7] + 1] *= 1.0 + 1e-6                             # one coupling no longer by-coordinate
+    d2[ip[7]] *= 1.0 + 1e-6                                 # row 7's vy-1 coupling: no longer by iy alone
     B = vk_lib.csr_matrix(sp.csr_matrix((d2, ix, ip), shape=(p.n, p.n)), ctx=gpu)
     assert B.grid4 == (0, 0, 0)
     S2 = twin.CONFIGS["S2"]

@@ -146,14 +146,17 @@ struct Tuning {
     int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
     int plain_grid = 2048;    // workgroups of the plain SELL SpMV
     int sell_swz = 0;         // SELL launches walk their groups in XCD-contiguous order
-    int plain_var = 0;        // plain SELL SpMV variant bits (k_sell VAR: 1 = padding gathers branched)
+    int plain_var = 1;        // plain SELL SpMV variant bits (k_sell VAR: 1 = padding gathers branched;
+                              // in-process A/B C3: 243.6 -> 221.3 us, the round-1 kernel's 218-222 us)
     int band_opt = 3;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
                               // C3: SpMV operands prefetched j00 254 -> 217 us, + three workgroups per
                               // CU for j <= 2: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms)
     int band_j3 = 2;          // ... bit 1 (three workgroups per CU) for steps j <= band_j3
     int lsv_spmv_cap = 8192;  // workgroups of the line path's table SpMV
-    int lsv_ring = 0;         // > 0: that table SpMV with x staged through LDS, ~that many workgroups
+    int lsv_ring = 2048;      // > 0: that table SpMV with x staged through LDS, ~that many workgroups
+                              // (in-process A/B, C3 line solve: 8.64 -> 8.26 ms; table SpMV 167 -> 105 us)
     int line_sweep = 0;       // > 0: line path update pass fused with the next table SpMV, ~that many workgroups
+                              // (with the ring SpMV on: 8.11 -> 8.19 ms at 512, slower at 256 / 1024: off)
     int ev_every = 1;         // host throttle event every this many Arnoldi steps (1..LOOKAHEAD+1)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
     int debug_band = 0;       // band-check trace on stderr

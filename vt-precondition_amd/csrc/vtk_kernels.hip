@@ -583,35 +583,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // (not in the plain SpMV: vtk_spmv, the measured standalone SpMV, never has lsv, and the
         // extra path cost its loop 249 -> 372 us on C3 through code shape alone)
         constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE && EPI != EPI_PLAIN;
-        constexpr bool G4_OK = (WU == 0 || WU == 9) && !PIPE && EPI != EPI_PLAIN;
+        constexpr bool G4_OK = (WU == 0 || WU == 9) && !PIPE && EPI != EPI_PLAIN && (VAR & 2) == 0;
         // the line-separable tables are a solver-launch form: compiled out of the plain SpMV (its
         // per-entry value selection cost the measured kernel 222 -> 242 us on C3)
         constexpr bool LSV_OK = EPI != EPI_PLAIN;
-        if (CANON_OK && a.canon) {
-            if (64 * q < a.n_local) {
-                const int L = a.lsv_L;
-                int xl = (64 * q) / L, v = 64 * q - xl * L + lane;
-                while (v >= L) {
-                    v -= L;
-                    ++xl;
-                }
-                int c[5];
-                double d[5];
-                if (act) {
-                    canon_row(a.lsv, a.n_local, L, a.lsv_lblk, xl, v, __builtin_nontemporal_load(a.lsv + row), c, d);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 5; ++u) {
-                        c[u] = -1;
-                        d[u] = 0.0;
-                    }
-                }
-                batch(c, d, [] {});
-            }
-        } else if (G4_OK && a.g4.tab != nullptr) {
-            // 4D grid rows (vtk::Grid4, checked bit for bit at setup): the nine couplings' columns
-            // from the row's coordinates, their values from D and the per-coordinate tables, summed
-            // in the stored (ascending column) order -- the SELL sum, without codes or values
+        // 4D grid rows (vtk::Grid4, checked bit for bit at setup): the nine couplings' columns
+        // from the row's coordinates, their values from D and the per-coordinate tables, summed
+        // in the stored (ascending column) order -- the SELL sum, without codes or values
+        auto g4_rows = [&]() {
             if (64 * q < a.n_local) {
                 const Grid4 &g = a.g4;
                 // coordinates: the chunk's first row by divisions (wave-uniform), then the lane
@@ -680,6 +659,35 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     }
                 }
             }
+        };
+        // G4ONLY (VAR bit 1): an instantiation with the grid-row form alone (no SELL code path
+        // competing for registers: the 9-wide C4 kernels spilled with both)
+        if constexpr ((VAR & 2) != 0) {
+            g4_rows();
+        } else
+        if (CANON_OK && a.canon) {
+            if (64 * q < a.n_local) {
+                const int L = a.lsv_L;
+                int xl = (64 * q) / L, v = 64 * q - xl * L + lane;
+                while (v >= L) {
+                    v -= L;
+                    ++xl;
+                }
+                int c[5];
+                double d[5];
+                if (act) {
+                    canon_row(a.lsv, a.n_local, L, a.lsv_lblk, xl, v, __builtin_nontemporal_load(a.lsv + row), c, d);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 5; ++u) {
+                        c[u] = -1;
+                        d[u] = 0.0;
+                    }
+                }
+                batch(c, d, [] {});
+            }
+        } else if (G4_OK && a.g4.tab != nullptr) {
+            g4_rows();
         } else if constexpr (WU > 0) {
             if (64 * q < a.n_local) {
                 constexpr int NWD = (WU + 7) / 8;   // 4-bit code words per lane
@@ -1079,7 +1087,8 @@ static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, 
         // 9-wide uniform rows (C4): the compile-time-width path (the cycle-start residual
         // kernel, 1440 us with the runtime loop)
         if (EPI != EPI_PREC_DC && VTK_SELL_WU && sell && bs == 8 && a.sell_uw == 9) {
-            hipLaunchKernelGGL((k_sell<VT, HALO, EPI, 8, true, 0, 9>), g, blk, 0, s, a);
+            if (a.g4.tab) hipLaunchKernelGGL((k_sell<VT, HALO, EPI, 8, true, 0, 9, 2>), g, blk, 0, s, a);
+            else hipLaunchKernelGGL((k_sell<VT, HALO, EPI, 8, true, 0, 9>), g, blk, 0, s, a);
             return hipGetLastError();
         }
         switch (bs) {
@@ -1175,7 +1184,8 @@ static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, 
         return hipGetLastError();
     }
     if (sell && bj.tri && bs == 8 && wu == 9) {
-        hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, VTK_DC_PSW9, 9>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        if (a.g4.tab) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, VTK_DC_PSW9, 9, 2>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        else hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, VTK_DC_PSW9, 9>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
         return hipGetLastError();
     }
     if (sell && bj.tri && bs == 8 && in.sell->nch > 0 && in.sell->entries <= in.sell->nch * 64 * 5) {
