@@ -178,6 +178,11 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
             x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)   # default: grid rows, dots fused
             assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
             assert np.array_equal(x1, x0), "grid rows change the bits"
+            for wgs in (1, 3, 4096):   # the split step's SpMV + BJ with x staged through LDS
+                with gpu.tuning(c4_fused=0, g4_ring=wgs):
+                    x3, i3, s3 = _solve(vk_lib, A, M, b, orth=orth)
+                assert i3 == 0 and s3.inner_iters == s1.inner_iters
+                assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs)
             if orth == "mgs":
                 assert np.array_equal(x1, x2)
             else:   # the fused dots sum in another fixed order: the DCGS2 bars

@@ -82,7 +82,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
-    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring},
 };
 
 const TuneKey *tune_key(const char *name) {
@@ -1078,7 +1078,10 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // there the SpMV + BJ kernel and the streaming dots kernel beat the register-capped fused
     // kernel (C4: 707 + 658 us vs 1473 us per step, 422 vs 405 it/s)
     // (with the 4D grid rows (Grid4) the fused kernel loads no values or codes: tuning c4_fused)
-    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused;   // C4 A/B: 213.8 -> 210.3 ms
+    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused && c->tune.g4_ring <= 0;   // C4 A/B: 213.8 -> 210.3 ms
+    // grid rows with x staged through LDS (k_g4_ring) for the split step's SpMV + BJ
+    const bool g4_ring = s.A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && s.A->use_sell && s.M &&
+                         s.M->kind == VTK_PREC_BJACOBI && s.M->bs == 8 && bj_op(s.M).tri != nullptr;
     const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M) && !g4_fused;
     const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9;
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
@@ -1197,6 +1200,11 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
               HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, s.p_of(j), s.dcpart, s.G, stop, j, c->stream)); }
             cnt = s.G;
+        } else if (g4_ring && wide9) {
+            TRY(halo_exchange(s.A, pj));
+            Prof pf(c, "spmv_bj", j, solver_matrix_bytes(s.A) + b_inv + 2 * n8);   // D, m, x, w
+            HIPCHK(c, launch_g4_ring(s.A->g4, pj, c->dist ? s.A->d_halo : nullptr, s.M->d_tri + s.M->tri_ld, s.w, n,
+                                     s.A->fp32, c->tune.g4_ring, stop, j, c->stream));
         } else {
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));

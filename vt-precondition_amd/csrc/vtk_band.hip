@@ -835,6 +835,139 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
     }
 }
 
+// 4D grid rows (vtk::Grid4) with x staged through LDS: w = M^-1 A p for the tridiagonal BJ(8)
+// (the split DCGS2 step of the 4D operators).  A workgroup of 256 lanes (one row
+// each) walks a contiguous range of 256-row groups; an LDS ring of G4R doubles holds x over
+// [g0 - S3, g0 + 256 + S3) (S3 = Nvx Nvy, the y-line), so the vy, vx and y couplings read LDS, and
+// the window slides by one group per step (the next group's 256 rows loaded one step ahead,
+// coalesced).  The x +- 1 plane couplings (S4 rows away) are contiguous 256-row blocks: two
+// coalesced loads per group (the workgroups 2.56 ranges away stream the same rows as their own
+// window at the same time: L2 / Infinity-Cache hits).  y couplings that wrap (iy = 0 / Ny - 1)
+// read x directly.  Terms summed in the stored order (as k_sell's grid rows), the BJ solve of
+// bj_trim_group: bit-identical to k_sell<EPI_PREC, 8, tri> on the same operator.
+constexpr int G4R = 8192;   // ring length (>= 2 S3 + 512), a power of two: 64 KB
+template <typename VT, bool HALO>
+__global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
+                                                const double *__restrict__ mtri, double *__restrict__ w, int n,
+                                                int ngroups_per_wg, const int *stop_col, int col) {
+    __shared__ double ring[G4R];
+    if (stopped(stop_col, col)) return;
+    const int tid = threadIdx.x, lane = tid & 63, ii = lane & 7;
+    const int S2 = g.Nvy, S3 = g.Nvx * g.Nvy, S4 = g.Ny * S3;
+    const int ng = (n + 255) / 256;
+    const int gb = blockIdx.x * ngroups_per_wg, ge = min(ng, gb + ngroups_per_wg);
+    if (gb >= ge) return;
+    const double *tb = g.tab;
+    const int oy = 2 * g.Nvx, ovx = oy + 2 * g.Nvy, ovy = ovx + 2 * g.X;
+    auto xat = [&](int c) { return (HALO && c >= n) ? halo[c - n] : x[c]; };
+    // the window's initial rows [gb 256 - S3, gb 256 + 256 + S3), clamped to [0, n)
+    const int w0 = gb * 256 - S3, w1 = gb * 256 + 256 + S3;
+    for (int r = w0 + tid; r < w1; r += NT)
+        if (r >= 0 && r < n) ring[r & (G4R - 1)] = x[r];
+    // per-group operands of the lane's row, loaded one group ahead
+    struct Ld {
+        double xn, xm, xp, m, d;
+    };
+    auto load = [&](int gi, Ld &o) {
+        const int r = gi * 256 + tid;
+        const int rc = r < n ? r : n - 1;
+        const int rn = gi * 256 + 256 + S3 + tid;   // the window's next row (for group gi + 1)
+        o.xn = rn < n ? x[rn] : 0.0;
+        // x -+ 1 planes of row rc (one rank: periodic inside the slab; else halo planes)
+        const int ix = rc / S4, rest = rc - ix * S4, X = n / S4;
+        int cm, cp;
+        if (g.lblk < 0) {
+            cm = (ix == 0 ? X - 1 : ix - 1) * S4 + rest;
+            cp = (ix == X - 1 ? 0 : ix + 1) * S4 + rest;
+        } else {
+            cm = ix >= 1 ? rc - S4 : n + g.lblk * S4 + rest;
+            cp = ix <= X - 2 ? rc + S4 : n + (1 - g.lblk) * S4 + rest;
+        }
+        o.xm = xat(cm);
+        o.xp = xat(cp);
+        o.m = __builtin_nontemporal_load(mtri + rc);
+        o.d = (double)__builtin_nontemporal_load(static_cast<const VT *>(g.D) + rc);
+    };
+    Ld nx;
+    load(gb, nx);
+    __syncthreads();
+    for (int gi = gb; gi < ge; ++gi) {
+        const Ld cu = nx;
+        if (gi + 1 < ge) load(gi + 1, nx);
+        const int r = gi * 256 + tid;
+        const bool act = r < n;
+        const int rc = act ? r : n - 1;
+        // coordinates of the row
+        const int jvy = rc % g.Nvy, t1 = rc / g.Nvy, jvx = t1 % g.Nvx, t2 = t1 / g.Nvx, iy = t2 % g.Ny, ix = t2 / g.Ny;
+        const bool pvm = jvx > 0, pvp = jvx < g.Nvx - 1, pym = jvy > 0, pyp = jvy < g.Nvy - 1;
+        // in-plane neighbours from the ring (y wraps read x directly)
+        const int cym = iy == 0 ? rc + (g.Ny - 1) * S3 : rc - S3;
+        const int cyp = iy == g.Ny - 1 ? rc - (g.Ny - 1) * S3 : rc + S3;
+        const double xym = iy == 0 ? x[cym] : ring[cym & (G4R - 1)];
+        const double xyp = iy == g.Ny - 1 ? x[cyp] : ring[cyp & (G4R - 1)];
+        const double xvm = ring[(rc - S2) & (G4R - 1)], xvp = ring[(rc + S2) & (G4R - 1)];
+        const double xwm = ring[(rc - 1) & (G4R - 1)], xwp = ring[(rc + 1) & (G4R - 1)];
+        const double x0 = ring[rc & (G4R - 1)];
+        const double t0 = tb[jvx] * cu.xm, t8 = tb[g.Nvx + jvx] * cu.xp;
+        const double t1y = tb[oy + jvy] * xym, t7 = tb[oy + g.Nvy + jvy] * xyp;
+        const double d2 = tb[ovx + ix], d6 = tb[ovx + g.X + ix], d3 = tb[ovy + iy], d5 = tb[ovy + g.Ny + iy];
+        const double t2v = d2 * xvm, t6 = d6 * xvp, t3 = d3 * xwm, t5 = d5 * xwp, t4 = cu.d * x0;
+        // the row's x -+ 1 plane columns, for the order of the wraps
+        const int X = n / S4, rest = rc - ix * S4;
+        int cm, cp;
+        if (g.lblk < 0) {
+            cm = (ix == 0 ? X - 1 : ix - 1) * S4 + rest;
+            cp = (ix == X - 1 ? 0 : ix + 1) * S4 + rest;
+        } else {
+            cm = ix >= 1 ? rc - S4 : n + g.lblk * S4 + rest;
+            cp = ix <= X - 2 ? rc + S4 : n + (1 - g.lblk) * S4 + rest;
+        }
+        double s = 0.0;
+        auto add2 = [&](bool pa, int ca, double ta, bool pb, int cb, double tb2) {
+            const bool sw = pa && pb && cb < ca;
+            const double u1 = sw ? tb2 : ta, u2 = sw ? ta : tb2;
+            const bool p1 = sw ? pb : pa, p2 = sw ? pa : pb;
+            s = p1 ? s + u1 : s;
+            s = p2 ? s + u2 : s;
+        };
+        add2(cm < rc, cm, t0, cp < rc, cp, t8);
+        add2(cym < rc, cym, t1y, cyp < rc, cyp, t7);
+        s = pvm ? s + t2v : s;
+        s = pym ? s + t3 : s;
+        s = s + t4;
+        s = pyp ? s + t5 : s;
+        s = pvp ? s + t6 : s;
+        add2(cym > rc, cym, t1y, cyp > rc, cyp, t7);
+        add2(cm > rc, cm, t0, cp > rc, cp, t8);
+        const double sub = (pym && ii > 0) ? 0.0 + d3 : 0.0, sup = (pyp && ii < 7) ? 0.0 + d5 : 0.0;
+        const double z = bj_trim_group<8>(act ? s : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
+        if (act) __builtin_nontemporal_store(z, w + r);
+        // slide the window: the rows of group gi + 1's upper edge (their slots held rows the
+        // remaining groups no longer read; the ring is > 2 S3 + 512 long)
+        const int rn = gi * 256 + 256 + S3 + tid;
+        if (rn < n) ring[rn & (G4R - 1)] = cu.xn;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
+                          int fp32, int wgs, const int *stop_col, int col, hipStream_t s) {
+    const int64_t S3 = (int64_t)g.Nvx * g.Nvy;
+    if (!g.tab || !g.D || 2 * S3 + 512 > G4R || n <= 0 || n > INT32_MAX / 2 || (halo == nullptr) != (g.lblk < 0))
+        return hipErrorInvalidValue;
+    const int64_t ng = (n + 255) / 256;
+    const int64_t per = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
+    const dim3 grid((unsigned)((ng + per - 1) / per)), blk(NT);
+    if (fp32) {
+        if (halo) hipLaunchKernelGGL((k_g4_ring<float, true>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
+        else hipLaunchKernelGGL((k_g4_ring<float, false>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
+    } else {
+        if (halo) hipLaunchKernelGGL((k_g4_ring<double, true>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
+        else hipLaunchKernelGGL((k_g4_ring<double, false>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
+    }
+    return hipGetLastError();
+}
+
 // the canonical table SpMV of line xl (one rank) from a ring of x lines: slots sm (x-1), sx (x),
 // sp (x+1), lane tid <-> position v; the same products in the same order as k_lsv_spmv<CANON>
 __device__ __forceinline__ double ring_line_spmv(const double *ring, int sm, int sx, int sp, int tid, int v, int L,

@@ -164,6 +164,8 @@ struct Tuning {
     int auto_band = 1;        // vtk_csr_create detects the line band (drop-in path)
     int grid4 = 1;            // solver launches read 4D grid rows from their coordinates (Grid4)
     int c4_fused = 1;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
+    int g4_ring = 0;          // > 0: the split step's SpMV + BJ of grid rows with x staged through LDS
+                              // (k_g4_ring, ~that many workgroups); takes precedence over c4_fused
 };
 }  // namespace vtk
 
@@ -508,6 +510,11 @@ struct LineSweepK {
     int n, L, H_parts;
 };
 hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s);
+// w = M^-1 A x for 4D grid rows with x staged through LDS (k_g4_ring): the tridiagonal BJ(8) of
+// m = mtri; about wgs workgroups, each a contiguous range of 256-row groups; halo != null: across
+// ranks (g.lblk the left plane's halo block).  Bit-identical to the SELL launch.
+hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
+                          int fp32, int wgs, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 
