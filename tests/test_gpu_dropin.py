@@ -178,11 +178,22 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
             x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)   # default: grid rows, dots fused
             assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
             assert np.array_equal(x1, x0), "grid rows change the bits"
-            for wgs in (1, 3, 4096):   # the split step's SpMV + BJ with x staged through LDS
-                with gpu.tuning(c4_fused=0, g4_ring=wgs):
+            # the split step's SpMV + BJ with x staged through LDS, operands 1..4 groups ahead
+            for wgs, pd in ((1, 3), (3, 1), (4096, 2), (7, 4)):
+                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_pd=pd):
                     x3, i3, s3 = _solve(vk_lib, A, M, b, orth=orth)
                 assert i3 == 0 and s3.inner_iters == s1.inner_iters
-                assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs)
+                assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs, pd)
+            # the ring with the step's dots fused in: the dots sum in another fixed order
+            with gpu.tuning(g4_ring=2048, g4_dc=1):
+                x4, i4, s4 = _solve(vk_lib, A, M, b, orth=orth)
+                x5, _, _ = _solve(vk_lib, A, M, b, orth=orth)
+            assert i4 == 0 and np.array_equal(x4, x5)
+            if orth == "mgs":
+                assert np.array_equal(x1, x4)
+            else:
+                assert abs(s4.inner_iters - s1.inner_iters) <= 1
+                assert np.linalg.norm(x4 - x1) / np.linalg.norm(x1) < 1e-9
             if orth == "mgs":
                 assert np.array_equal(x1, x2)
             else:   # the fused dots sum in another fixed order: the DCGS2 bars

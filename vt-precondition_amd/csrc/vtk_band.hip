@@ -837,91 +837,142 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
 
 // 4D grid rows (vtk::Grid4) with x staged through LDS: w = M^-1 A p for the tridiagonal BJ(8)
 // (the split DCGS2 step of the 4D operators).  A workgroup of 256 lanes (one row
-// each) walks a contiguous range of 256-row groups; an LDS ring of G4R doubles holds x over
+// each) walks a contiguous range of 256-row groups; an LDS ring of RL doubles holds x over
 // [g0 - S3, g0 + 256 + S3) (S3 = Nvx Nvy, the y-line), so the vy, vx and y couplings read LDS, and
-// the window slides by one group per step (the next group's 256 rows loaded one step ahead,
-// coalesced).  The x +- 1 plane couplings (S4 rows away) are contiguous 256-row blocks: two
-// coalesced loads per group (the workgroups 2.56 ranges away stream the same rows as their own
-// window at the same time: L2 / Infinity-Cache hits).  y couplings that wrap (iy = 0 / Ny - 1)
-// read x directly.  Terms summed in the stored order (as k_sell's grid rows), the BJ solve of
-// bj_trim_group: bit-identical to k_sell<EPI_PREC, 8, tri> on the same operator.
-constexpr int G4R = 8192;   // ring length (>= 2 S3 + 512), a power of two: 64 KB
-template <typename VT, bool HALO>
+// the window slides by one group per step.  Every global operand of a group -- the window's next
+// 256 rows, the x -+ 1 plane rows (S4 away: contiguous 256-row blocks), the y-wrap row, m and D --
+// is loaded PD groups ahead into a register queue, all loads unconditional (clamped rows, the
+// halo chosen by address): no exec-masked load, so the wait for a group's operands does not wait
+// for the groups behind it.  Coordinates advance by 256 in the mixed radix (no division per row),
+// ring slots by 256 modulo RL.  Terms summed in the stored order (as k_sell's grid rows), the BJ
+// solve of bj_trim_group: bit-identical to k_sell<EPI_PREC, 8, tri> on the same operator.
+// RL: ring length (>= 2 S3 + 512): 4608 (36 KB, four workgroups per CU) when the y-line allows
+// (C4: S3 = 2000), else 8192 (64 KB); the tables TX | TY | TVX | TVY (<= G4TAB doubles) in LDS
+// too: three workgroups per CU at C4.
+// DC: the DCGS2 step j fused in (x = p_j = V[j]): s = V_j^T p, z = V_j^T w, |p|^2, p.w, |w|^2 per
+// workgroup in launch_dc_dots' partial layout.  Each group's p and w are staged in LDS (two
+// buffers) and wave wv reads the group's rows of V[k], k = wv, wv + 4, ... (the split of
+// dc_rows); the w write stays (the update pass reads it).
+constexpr int G4TAB = 1024;
+template <typename VT, bool HALO, int RL, int PD, bool DC>
 __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
                                                 const double *__restrict__ mtri, double *__restrict__ w, int n,
-                                                int ngroups_per_wg, const int *stop_col, int col) {
-    __shared__ double ring[G4R];
+                                                int ngroups_per_wg, G4Dots dd, const int *stop_col, int col) {
+    __shared__ double ring[RL];
+    __shared__ double tb[G4TAB];
+    constexpr int KPW = DC_MAXJ / (NT / 64);
+    __shared__ double pw[DC ? 2 : 1][DC ? 2 * NT : 1];
+    double ds_[KPW], dz_[KPW], daa = 0.0, dab = 0.0, dag = 0.0;
+#pragma unroll
+    for (int u = 0; u < KPW; ++u) ds_[u] = dz_[u] = 0.0;
     if (stopped(stop_col, col)) return;
     const int tid = threadIdx.x, lane = tid & 63, ii = lane & 7;
-    const int S2 = g.Nvy, S3 = g.Nvx * g.Nvy, S4 = g.Ny * S3;
+    const int Nvy = g.Nvy, Nvx = g.Nvx, Ny = g.Ny;
+    const int S2 = Nvy, S3 = Nvx * Nvy, S4 = Ny * S3;
     const int ng = (n + 255) / 256;
     const int gb = blockIdx.x * ngroups_per_wg, ge = min(ng, gb + ngroups_per_wg);
     if (gb >= ge) return;
-    const double *tb = g.tab;
-    const int oy = 2 * g.Nvx, ovx = oy + 2 * g.Nvy, ovy = ovx + 2 * g.X;
-    auto xat = [&](int c) { return (HALO && c >= n) ? halo[c - n] : x[c]; };
+    const int oy = 2 * Nvx, ovx = oy + 2 * Nvy, ovy = ovx + 2 * g.X;
+    const int lb = g.lblk;
+    // the value tables in LDS (a table load in the row loop would be a global load issued after
+    // the queue's prefetch: waiting for it would wait for the whole queue)
+    for (int i = tid; i < ovy + 2 * Ny; i += NT) tb[i] = g.tab[i];
     // the window's initial rows [gb 256 - S3, gb 256 + 256 + S3), clamped to [0, n)
-    const int w0 = gb * 256 - S3, w1 = gb * 256 + 256 + S3;
-    for (int r = w0 + tid; r < w1; r += NT)
-        if (r >= 0 && r < n) ring[r & (G4R - 1)] = x[r];
-    // per-group operands of the lane's row, loaded one group ahead
-    struct Ld {
-        double xn, xm, xp, m, d;
+    for (int r = gb * 256 - S3 + tid; r < gb * 256 + 256 + S3; r += NT)
+        if (r >= 0 && r < n) ring[r % RL] = x[r];
+    // 256 in the mixed radix (Nvy, Nvx, Ny, X)
+    const int a0 = 256 % Nvy, q0 = 256 / Nvy, a1 = q0 % Nvx, q1 = q0 / Nvx, a2 = q1 % Ny, a3 = q1 / Ny;
+    struct Co {
+        int jvy, jvx, iy, ix;
     };
-    auto load = [&](int gi, Ld &o) {
-        const int r = gi * 256 + tid;
-        const int rc = r < n ? r : n - 1;
-        const int rn = gi * 256 + 256 + S3 + tid;   // the window's next row (for group gi + 1)
-        o.xn = rn < n ? x[rn] : 0.0;
-        // x -+ 1 planes of row rc (one rank: periodic inside the slab; else halo planes)
-        const int ix = rc / S4, rest = rc - ix * S4, X = n / S4;
-        int cm, cp;
-        if (g.lblk < 0) {
-            cm = (ix == 0 ? X - 1 : ix - 1) * S4 + rest;
-            cp = (ix == X - 1 ? 0 : ix + 1) * S4 + rest;
+    auto adv = [&](Co &c) {
+        c.jvy += a0;
+        int cy = c.jvy >= Nvy;
+        c.jvy -= cy ? Nvy : 0;
+        c.jvx += a1 + cy;
+        cy = c.jvx >= Nvx;
+        c.jvx -= cy ? Nvx : 0;
+        c.iy += a2 + cy;
+        cy = c.iy >= Ny;
+        c.iy -= cy ? Ny : 0;
+        c.ix += a3 + cy;
+    };
+    // the x -+ 1 plane columns of row rc (one rank: periodic inside the slab; else halo planes)
+    auto xcols = [&](int rc, int &cm, int &cp) {
+        if (!HALO) {
+            cm = rc >= S4 ? rc - S4 : rc + (n - S4);
+            cp = rc < n - S4 ? rc + S4 : rc - (n - S4);
         } else {
-            cm = ix >= 1 ? rc - S4 : n + g.lblk * S4 + rest;
-            cp = ix <= X - 2 ? rc + S4 : n + (1 - g.lblk) * S4 + rest;
+            cm = rc >= S4 ? rc - S4 : n + lb * S4 + rc;
+            cp = rc < n - S4 ? rc + S4 : (1 - lb) * S4 + rc + S4;
         }
+    };
+    auto xat = [&](int c) { return HALO ? *(c >= n ? halo + (c - n) : x + c) : x[c]; };
+    struct Ld {
+        double xn, xm, xp, xw, m, d;
+        Co c;
+    };
+    Co lead;
+    {
+        const int r = gb * 256 + tid;
+        lead.jvy = r % Nvy;
+        const int t1 = r / Nvy;
+        lead.jvx = t1 % Nvx;
+        const int t2 = t1 / Nvx;
+        lead.iy = t2 % Ny;
+        lead.ix = t2 / Ny;
+    }
+    auto load = [&](int gl, Ld &o) {
+        const int r = gl * 256 + tid;
+        const int rc = min(r, n - 1);
+        o.xn = x[min(r + 256 + S3, n - 1)];
+        int cm, cp;
+        xcols(rc, cm, cp);
         o.xm = xat(cm);
         o.xp = xat(cp);
+        const int cw = lead.iy == 0 ? rc + (Ny - 1) * S3 : (lead.iy == Ny - 1 ? rc - (Ny - 1) * S3 : rc);
+        o.xw = x[min(max(cw, 0), n - 1)];
         o.m = __builtin_nontemporal_load(mtri + rc);
         o.d = (double)__builtin_nontemporal_load(static_cast<const VT *>(g.D) + rc);
+        o.c = lead;
+        adv(lead);
     };
-    Ld nx;
-    load(gb, nx);
+    Ld qu[PD];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) load(gb + k, qu[k]);
+    int sb = (gb * 256 + tid) % RL;   // ring slot of the lane's row
+    auto slot = [&](int off) {
+        int t = sb + off;
+        t += t < 0 ? RL : 0;
+        t -= t >= RL ? RL : 0;
+        return t;
+    };
     __syncthreads();
     for (int gi = gb; gi < ge; ++gi) {
-        const Ld cu = nx;
-        if (gi + 1 < ge) load(gi + 1, nx);
+        const Ld cu = qu[0];
+#pragma unroll
+        for (int k = 0; k + 1 < PD; ++k) qu[k] = qu[k + 1];
+        load(gi + PD, qu[PD - 1]);
         const int r = gi * 256 + tid;
         const bool act = r < n;
         const int rc = act ? r : n - 1;
-        // coordinates of the row
-        const int jvy = rc % g.Nvy, t1 = rc / g.Nvy, jvx = t1 % g.Nvx, t2 = t1 / g.Nvx, iy = t2 % g.Ny, ix = t2 / g.Ny;
-        const bool pvm = jvx > 0, pvp = jvx < g.Nvx - 1, pym = jvy > 0, pyp = jvy < g.Nvy - 1;
-        // in-plane neighbours from the ring (y wraps read x directly)
-        const int cym = iy == 0 ? rc + (g.Ny - 1) * S3 : rc - S3;
-        const int cyp = iy == g.Ny - 1 ? rc - (g.Ny - 1) * S3 : rc + S3;
-        const double xym = iy == 0 ? x[cym] : ring[cym & (G4R - 1)];
-        const double xyp = iy == g.Ny - 1 ? x[cyp] : ring[cyp & (G4R - 1)];
-        const double xvm = ring[(rc - S2) & (G4R - 1)], xvp = ring[(rc + S2) & (G4R - 1)];
-        const double xwm = ring[(rc - 1) & (G4R - 1)], xwp = ring[(rc + 1) & (G4R - 1)];
-        const double x0 = ring[rc & (G4R - 1)];
-        const double t0 = tb[jvx] * cu.xm, t8 = tb[g.Nvx + jvx] * cu.xp;
-        const double t1y = tb[oy + jvy] * xym, t7 = tb[oy + g.Nvy + jvy] * xyp;
-        const double d2 = tb[ovx + ix], d6 = tb[ovx + g.X + ix], d3 = tb[ovy + iy], d5 = tb[ovy + g.Ny + iy];
+        const int jvy = cu.c.jvy, jvx = cu.c.jvx, iy = cu.c.iy, ix = cu.c.ix;
+        const bool pvm = jvx > 0, pvp = jvx < Nvx - 1, pym = jvy > 0, pyp = jvy < Nvy - 1;
+        // in-plane neighbours from the ring (y wraps from the queue)
+        const int cym = iy == 0 ? rc + (Ny - 1) * S3 : rc - S3;
+        const int cyp = iy == Ny - 1 ? rc - (Ny - 1) * S3 : rc + S3;
+        const double xym = iy == 0 ? cu.xw : ring[slot(-S3)];
+        const double xyp = iy == Ny - 1 ? cu.xw : ring[slot(S3)];
+        const double xvm = ring[slot(-S2)], xvp = ring[slot(S2)];
+        const double xwm = ring[slot(-1)], xwp = ring[slot(1)];
+        const double x0 = ring[sb];
+        const int jx = min(jvx, Nvx - 1), jy = min(jvy, Nvy - 1), kx = min(ix, g.X - 1), ky = min(iy, Ny - 1);
+        const double t0 = tb[jx] * cu.xm, t8 = tb[Nvx + jx] * cu.xp;
+        const double t1y = tb[oy + jy] * xym, t7 = tb[oy + Nvy + jy] * xyp;
+        const double d2 = tb[ovx + kx], d6 = tb[ovx + g.X + kx], d3 = tb[ovy + ky], d5 = tb[ovy + Ny + ky];
         const double t2v = d2 * xvm, t6 = d6 * xvp, t3 = d3 * xwm, t5 = d5 * xwp, t4 = cu.d * x0;
-        // the row's x -+ 1 plane columns, for the order of the wraps
-        const int X = n / S4, rest = rc - ix * S4;
         int cm, cp;
-        if (g.lblk < 0) {
-            cm = (ix == 0 ? X - 1 : ix - 1) * S4 + rest;
-            cp = (ix == X - 1 ? 0 : ix + 1) * S4 + rest;
-        } else {
-            cm = ix >= 1 ? rc - S4 : n + g.lblk * S4 + rest;
-            cp = ix <= X - 2 ? rc + S4 : n + (1 - g.lblk) * S4 + rest;
-        }
+        xcols(rc, cm, cp);
         double s = 0.0;
         auto add2 = [&](bool pa, int ca, double ta, bool pb, int cb, double tb2) {
             const bool sw = pa && pb && cb < ca;
@@ -942,29 +993,107 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
         const double sub = (pym && ii > 0) ? 0.0 + d3 : 0.0, sup = (pyp && ii < 7) ? 0.0 + d5 : 0.0;
         const double z = bj_trim_group<8>(act ? s : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
         if (act) __builtin_nontemporal_store(z, w + r);
+        const int buf = gi & 1;
+        if constexpr (DC) {
+            pw[buf][tid] = act ? x0 : 0.0;
+            pw[buf][NT + tid] = act ? z : 0.0;
+        }
         // slide the window: the rows of group gi + 1's upper edge (their slots held rows the
         // remaining groups no longer read; the ring is > 2 S3 + 512 long)
-        const int rn = gi * 256 + 256 + S3 + tid;
-        if (rn < n) ring[rn & (G4R - 1)] = cu.xn;
+        if (r + 256 + S3 < n) ring[slot(256 + S3)] = cu.xn;
+        sb = slot(256);
         __syncthreads();
+        if constexpr (DC) {
+            // the group's dots (the other buffer is written next; this one again only after the
+            // next barrier, which every wave reaches after these reads)
+            const int wv = tid >> 6;
+            const double *pt = pw[buf], *wt = pw[buf] + NT;
+#pragma unroll
+            for (int u = 0; u < KPW; ++u) {
+                const int k = wv + u * (NT / 64);
+                if (k < dd.j) {
+                    const double *vk = dd.V + (size_t)k * dd.ld;
+#pragma unroll
+                    for (int h = 0; h < NT / 64; ++h) {
+                        const int i = lane + 64 * h;
+                        const double v = __builtin_nontemporal_load(vk + min(gi * 256 + i, n - 1));
+                        ds_[u] += v * pt[i];
+                        dz_[u] += v * wt[i];
+                    }
+                }
+            }
+            if (wv == 0) {
+#pragma unroll
+                for (int h = 0; h < NT / 64; ++h) {
+                    const int i = lane + 64 * h;
+                    daa += pt[i] * pt[i];
+                    dab += pt[i] * wt[i];
+                    dag += wt[i] * wt[i];
+                }
+            }
+        }
+    }
+    if constexpr (DC) {
+        // per-workgroup partials (dc_write's layout); the ring is free now
+        const int wv = tid >> 6;
+        double *red = ring;
+#pragma unroll
+        for (int u = 0; u < KPW; ++u) {
+            const int k = wv + u * (NT / 64);
+            const double ts = wave_sum(ds_[u]), tz = wave_sum(dz_[u]);
+            if (lane == 0 && k < dd.j) { red[k] = ts; red[DC_MAXJ + k] = tz; }
+        }
+        const double t0 = wave_sum(daa), t1 = wave_sum(dab), t2 = wave_sum(dag);
+        if (wv == 0 && lane == 0) { red[2 * DC_MAXJ] = t0; red[2 * DC_MAXJ + 1] = t1; red[2 * DC_MAXJ + 2] = t2; }
+        __syncthreads();
+        for (int q = tid; q < DC_NQ; q += NT) {
+            const bool used = q < dd.j || (q >= DC_MAXJ && q < DC_MAXJ + dd.j) || q >= 2 * DC_MAXJ;
+            if (used) dd.part[(size_t)q * GMAX + blockIdx.x] = red[q];
+        }
     }
 }
 
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
-                          int fp32, int wgs, const int *stop_col, int col, hipStream_t s) {
-    const int64_t S3 = (int64_t)g.Nvx * g.Nvy;
-    if (!g.tab || !g.D || 2 * S3 + 512 > G4R || n <= 0 || n > INT32_MAX / 2 || (halo == nullptr) != (g.lblk < 0))
+                          int fp32, int wgs, int pd, int xcd, const G4Dots *dots, int *grid_out, const int *stop_col,
+                          int col, hipStream_t s) {
+    const int64_t S3 = (int64_t)g.Nvx * g.Nvy, S4 = S3 * g.Ny;
+    if (!g.tab || !g.D || 2 * S3 + 512 > 8192 || n <= 0 || n > INT32_MAX / 2 || S4 <= 0 || n % S4 ||
+        2 * (g.Nvx + g.Nvy + g.X + g.Ny) > G4TAB ||
+        (halo == nullptr) != (g.lblk < 0))
         return hipErrorInvalidValue;
+    const bool small = 2 * S3 + 512 <= 4608;
     const int64_t ng = (n + 255) / 256;
-    const int64_t per = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
+    int64_t per = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
+    // xcd > 0: ranges of S4 / xcd rows, so that the ranges reading a range's rows as their x -+ 1
+    // planes are xcd workgroups away -- on the same XCD (workgroups are dealt round-robin over the
+    // eight XCDs) when xcd is a multiple of 8: those reads hit that XCD's L2
+    if (xcd > 0) per = std::max<int64_t>(1, (S4 + 128 * xcd) / (256 * (int64_t)xcd));
+    // the fused dots write one partial per workgroup: at most GMAX workgroups
+    if (dots) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
     const dim3 grid((unsigned)((ng + per - 1) / per)), blk(NT);
+    if (dots && (dots->j < 0 || dots->j > DC_MAXJ || !dots->V || !dots->part)) return hipErrorInvalidValue;
+    if (grid_out) *grid_out = (int)grid.x;
+    const G4Dots dd = dots ? *dots : G4Dots{};
+#define VTK_G4R(VT_, H_, RL_, PD_, DC_) \
+    hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, PD_, DC_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, dd, \
+                       stop_col, col)
+#define VTK_G4R_PD(VT_, H_, RL_) \
+    do { \
+        if (dots) VTK_G4R(VT_, H_, RL_, 1, true); \
+        else if (pd <= 1) VTK_G4R(VT_, H_, RL_, 1, false); \
+        else if (pd == 2) VTK_G4R(VT_, H_, RL_, 2, false); \
+        else if (pd == 3) VTK_G4R(VT_, H_, RL_, 3, false); \
+        else VTK_G4R(VT_, H_, RL_, 4, false); \
+    } while (0)
     if (fp32) {
-        if (halo) hipLaunchKernelGGL((k_g4_ring<float, true>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
-        else hipLaunchKernelGGL((k_g4_ring<float, false>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
+        if (halo) { if (small) VTK_G4R_PD(float, true, 4608); else VTK_G4R_PD(float, true, 8192); }
+        else { if (small) VTK_G4R_PD(float, false, 4608); else VTK_G4R_PD(float, false, 8192); }
     } else {
-        if (halo) hipLaunchKernelGGL((k_g4_ring<double, true>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
-        else hipLaunchKernelGGL((k_g4_ring<double, false>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, stop_col, col);
+        if (halo) { if (small) VTK_G4R_PD(double, true, 4608); else VTK_G4R_PD(double, true, 8192); }
+        else { if (small) VTK_G4R_PD(double, false, 4608); else VTK_G4R_PD(double, false, 8192); }
     }
+#undef VTK_G4R_PD
+#undef VTK_G4R
     return hipGetLastError();
 }
 

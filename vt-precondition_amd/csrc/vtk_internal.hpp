@@ -166,6 +166,9 @@ struct Tuning {
     int c4_fused = 1;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
     int g4_ring = 0;          // > 0: the split step's SpMV + BJ of grid rows with x staged through LDS
                               // (k_g4_ring, ~that many workgroups); takes precedence over c4_fused
+    int g4_pd = 1;            // k_g4_ring: groups of operands loaded ahead (1..4)
+    int g4_xcd = 0;           // k_g4_ring: > 0: ranges of S4 / g4_xcd rows (overrides g4_ring's count)
+    int g4_dc = 0;            // k_g4_ring: the DCGS2 step's dots fused in
 };
 }  // namespace vtk
 
@@ -512,9 +515,18 @@ struct LineSweepK {
 hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s);
 // w = M^-1 A x for 4D grid rows with x staged through LDS (k_g4_ring): the tridiagonal BJ(8) of
 // m = mtri; about wgs workgroups, each a contiguous range of 256-row groups; halo != null: across
-// ranks (g.lblk the left plane's halo block).  Bit-identical to the SELL launch.
+// ranks (g.lblk the left plane's halo block).  Bit-identical to the SELL launch.  dots != null:
+// DCGS2 step dots->j fused in (x = V[j]), partials per workgroup (launch_dc_dots' layout; at most
+// GMAX workgroups, the count in *grid_out).
+struct G4Dots {
+    const double *V = nullptr;
+    int64_t ld = 0;
+    int j = 0;
+    double *part = nullptr;
+};
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
-                          int fp32, int wgs, const int *stop_col, int col, hipStream_t s);
+                          int fp32, int wgs, int pd, int xcd, const G4Dots *dots, int *grid_out, const int *stop_col,
+                          int col, hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 
