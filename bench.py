@@ -425,11 +425,20 @@ def main():
             tt = torch.tensor([el_l], dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el_l = float(tt.item())
+        # one profiled line solve: per-class launches, mean time and rate
+        ctx.profile(True)
+        vk.gmres(A, b, rtol=args.rtol, restart=args.restart, M=ML)
+        kprof_l = ctx.profile_read()
+        ctx.profile(False)
+        tot_l = sum(v["seconds"] for v in kprof_l.values()) or 1.0
         ML.close()
         alt = {"prec": f"Line({args.seg}), compact apply", "info": inf_l,
                "inner_iters_per_solve": it_l / reps_l, "ms_per_solve": el_l / reps_l * 1e3,
                "iters_per_s": it_l / el_l,
-               "time_to_solution_speedup_vs_bj": (elapsed / args.steps) / (el_l / reps_l)}
+               "time_to_solution_speedup_vs_bj": (elapsed / args.steps) / (el_l / reps_l),
+               "kernels": {k: {"avg_us": round(v["avg_us"], 2), "gbs": round(v["gbs"], 1),
+                               "launches": v["launches"], "share": round(v["seconds"] / tot_l, 4)}
+                           for k, v in sorted(kprof_l.items(), key=lambda kv: -kv[1]["seconds"])}}
 
     ms = elapsed / args.steps * 1e3
     # ---- reconciliation with SURVEY §8(d)'s byte model (MGS, inverse BJ(bs), CSR int32 columns):

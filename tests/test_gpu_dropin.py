@@ -171,11 +171,12 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
     for A in (G, U):
         M = vk_lib.block_jacobi(A, 8)
         for orth in ("dcgs2", "mgs"):
-            with gpu.tuning(c4_fused=0):   # the split step (SpMV + BJ, then the dots)
+            with gpu.tuning(c4_fused=0, g4_ring=0):   # the split step (SELL SpMV + BJ, then the dots)
                 x1, i1, s1 = _solve(vk_lib, A, M, b, orth=orth)
             with gpu.tuning(grid4=0):      # ... reading the SELL values and codes
                 x0, i0, s0 = _solve(vk_lib, A, M, b, orth=orth)
-            x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)   # default: grid rows, dots fused
+            with gpu.tuning(g4_ring=0):    # grid rows, dots fused into the SELL kernel
+                x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)
             assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
             assert np.array_equal(x1, x0), "grid rows change the bits"
             # the split step's SpMV + BJ with x staged through LDS, operands 1..4 groups ahead
@@ -184,6 +185,8 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
                     x3, i3, s3 = _solve(vk_lib, A, M, b, orth=orth)
                 assert i3 == 0 and s3.inner_iters == s1.inner_iters
                 assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs, pd)
+            xd, _, sd = _solve(vk_lib, A, M, b, orth=orth)   # default: the ring split step
+            assert sd.inner_iters == s1.inner_iters and np.array_equal(x1, xd)
             # the ring with the step's dots fused in: the dots sum in another fixed order
             with gpu.tuning(g4_ring=2048, g4_dc=1):
                 x4, i4, s4 = _solve(vk_lib, A, M, b, orth=orth)

@@ -34,6 +34,12 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
     hc = ctx.comm_init_host(rank, world)
     p = twin.CONFIGS[case]
     align = p.shape[-1] if p.dim == 2 else (8 if p.dim == 1 else p.shape[-1] * p.shape[-2])
+    planes = isinstance(from_host, str) and from_host.startswith("planes")
+    if planes:   # slabs of whole x planes: the 4D grid rows hold across ranks (halo planes)
+        align = p.shape[1] * p.shape[2] * p.shape[3]
+        if from_host == "planes_ring":   # the LDS-ring step with the dots fused, across ranks
+            ctx.set_tuning("g4_ring", 64)
+            ctx.set_tuning("g4_dc", 1)
     offs = vk.partition_rows(p.n, world, align)
     rb, re_ = int(offs[rank]), int(offs[rank + 1])
     if from_host == "npz":   # this rank's row block of a SciPy archive (vtkrylov.load_npz)
@@ -43,6 +49,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
         A = vk.csr_matrix((d, ix, ip), shape=(p.n, p.n), ctx=ctx, offsets=offs)
     else:           # device assembly of this rank's rows
         A = vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=ctx, offsets=offs)
+    if planes:
+        assert A.grid4 == tuple(p.shape[1:]), A.grid4
     # the line band is found in the CSR on every path (device assembly, host row blocks, npz)
     assert A.line_band == (p.shape[1] if p.dim == 2 else 0), A.line_band
     x = twin.rhs(p.n, seed=0xC0FFEE)
@@ -65,7 +73,9 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
                                                        ("S2", 3, True, "dcgs2"), ("S4", 2, "npz", "dcgs2"),
                                                        ("C1", 2, False, "mgs"),
                                                        ("C1", 2, False, "dcgs2"), ("C1", 3, False, "dcgs2"),
-                                                       ("S2", 2, True, "dcgs2"), ("S2", 4, False, "dcgs2")])
+                                                       ("S2", 2, True, "dcgs2"), ("S2", 4, False, "dcgs2"),
+                                                       ("S4", 3, "planes", "dcgs2"), ("S4", 2, "planes_ring", "dcgs2"),
+                                                       ("S4", 3, "planes_ring", "dcgs2"), ("S4F", 2, "planes_ring", "mgs")])
 def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 

@@ -906,7 +906,10 @@ int grid4_set(vtk_csr *A, int64_t Ny, int64_t Nvx, int64_t Nvy) {
         bool solo = true;
         BandLayout lay;
         if (band_check_dist(A, S4, solo, lay) != VTK_OK) return VTK_ERR_ARG;
-        if (!solo) g.lblk = lay.lblk;
+        if (!solo) {
+            g.lblk = lay.lblk;
+            g.xord = (A->row_begin == 0 ? 1 : 0) | (A->row_end == A->n_global ? 2 : 0);
+        }
     }
     if (g.lblk < 0 && g.X < 3) return VTK_ERR_ARG;
     DBuf tab, D, bad;

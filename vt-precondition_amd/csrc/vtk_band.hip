@@ -653,11 +653,13 @@ __global__ __launch_bounds__(NT) void k_grid4_build(const int32_t *__restrict__ 
         int64_t c[9];
         bool p[9];
         g4_cols(r, q, g, n, c, p);
+        int64_t key[9];   // stored-order positions (halo planes: Grid4::xord)
+        for (int k = 0; k < 9; ++k) key[k] = k == 0 || k == 8 ? g4_key(c[k], k, n, g) : c[k];
         int ord[9], m = 0;
         for (int k = 0; k < 9; ++k)
             if (p[k]) ord[m++] = k;
-        for (int i = 1; i < m; ++i)   // ascending columns (the stored order of a canonical CSR)
-            for (int t = i; t > 0 && c[ord[t]] < c[ord[t - 1]]; --t) {
+        for (int i = 1; i < m; ++i)   // ascending global columns (the stored order of a canonical CSR)
+            for (int t = i; t > 0 && key[ord[t]] < key[ord[t - 1]]; --t) {
                 const int s = ord[t];
                 ord[t] = ord[t - 1];
                 ord[t - 1] = s;
@@ -973,15 +975,16 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
         const double t2v = d2 * xvm, t6 = d6 * xvp, t3 = d3 * xwm, t5 = d5 * xwp, t4 = cu.d * x0;
         int cm, cp;
         xcols(rc, cm, cp);
+        const int64_t km = g4_key(cm, 0, n, g), kp = g4_key(cp, 8, n, g);   // stored-order positions
         double s = 0.0;
-        auto add2 = [&](bool pa, int ca, double ta, bool pb, int cb, double tb2) {
+        auto add2 = [&](bool pa, int64_t ca, double ta, bool pb, int64_t cb, double tb2) {
             const bool sw = pa && pb && cb < ca;
             const double u1 = sw ? tb2 : ta, u2 = sw ? ta : tb2;
             const bool p1 = sw ? pb : pa, p2 = sw ? pa : pb;
             s = p1 ? s + u1 : s;
             s = p2 ? s + u2 : s;
         };
-        add2(cm < rc, cm, t0, cp < rc, cp, t8);
+        add2(km < rc, km, t0, kp < rc, kp, t8);
         add2(cym < rc, cym, t1y, cyp < rc, cyp, t7);
         s = pvm ? s + t2v : s;
         s = pym ? s + t3 : s;
@@ -989,7 +992,7 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
         s = pyp ? s + t5 : s;
         s = pvp ? s + t6 : s;
         add2(cym > rc, cym, t1y, cyp > rc, cyp, t7);
-        add2(cm > rc, cm, t0, cp > rc, cp, t8);
+        add2(km > rc, km, t0, kp > rc, kp, t8);
         const double sub = (pym && ii > 0) ? 0.0 + d3 : 0.0, sup = (pyp && ii < 7) ? 0.0 + d5 : 0.0;
         const double z = bj_trim_group<8>(act ? s : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
         if (act) __builtin_nontemporal_store(z, w + r);

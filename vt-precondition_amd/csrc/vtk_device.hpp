@@ -124,6 +124,15 @@ __device__ __forceinline__ void g4_cols(int64_t r, const G4Row &q, const Grid4 &
     p[5] = q.jvy < g.Nvy - 1;
 }
 
+// a grid column's position in the row's stored order: local columns as they are; a halo plane's
+// column (k = 0: the x - 1 plane, 8: x + 1) before or after every local one (Grid4::xord)
+__device__ __forceinline__ int64_t g4_key(int64_t c, int k, int64_t n, const Grid4 &g) {
+    if (c < n) return c;
+    constexpr int64_t BIG = (int64_t)1 << 40;
+    const bool after = k == 0 ? (g.xord & 1) != 0 : (g.xord & 2) == 0;
+    return after ? BIG + c : c - BIG;
+}
+
 // Bijective XCD swizzle (cdna_hip_programming.md T1): workgroups are dealt round-robin over the
 // 8 XCDs, so b and b + 8 share an L2.  The logical id gives the blocks sharing an XCD one
 // contiguous id range; with the grid-stride tile loop an XCD then works on a contiguous window

@@ -127,6 +127,10 @@ struct LineOp {
 struct Grid4 {
     int Ny = 0, Nvx = 0, Nvy = 0, X = 0;
     int lblk = -1;
+    // across ranks, where the halo planes' columns sit in a row's stored (global column) order:
+    // bit 0: the left plane's after the row (the slab starts at plane 0: its left is the last
+    // plane), bit 1: the right plane's before it (the slab ends at the last plane)
+    int xord = 0;
     const double *tab = nullptr;   // TX[2][Nvx] | TY[2][Nvy] | TVX[2][X] | TVY[2][Ny] (-, + each)
     const void *D = nullptr;       // diagonal per row, the operator's value type
 };
@@ -164,7 +168,7 @@ struct Tuning {
     int auto_band = 1;        // vtk_csr_create detects the line band (drop-in path)
     int grid4 = 1;            // solver launches read 4D grid rows from their coordinates (Grid4)
     int c4_fused = 1;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
-    int g4_ring = 0;          // > 0: the split step's SpMV + BJ of grid rows with x staged through LDS
+    int g4_ring = 2048;       // > 0: the split step's SpMV + BJ of grid rows with x staged through LDS
                               // (k_g4_ring, ~that many workgroups); takes precedence over c4_fused
     int g4_pd = 1;            // k_g4_ring: groups of operands loaded ahead (1..4)
     int g4_xcd = 0;           // k_g4_ring: > 0: ranges of S4 / g4_xcd rows (overrides g4_ring's count)

@@ -641,10 +641,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     s = p1 ? s + t1 : s;
                     s = p2 ? s + t2 : s;
                 };
+                // the x planes' positions in the stored order (halo planes: Grid4::xord)
+                const int64_t k0 = g4_key(c9[0], 0, a.n_local, g), k8 = g4_key(c9[8], 8, a.n_local, g);
                 if (act) {
                     // x planes before the row's plane, then y lines before its line (periodic
                     // wraps), the in-line block, the y lines and x planes after
-                    add2(c9[0] < row, c9[0], tk[0], c9[8] < row, c9[8], tk[8]);
+                    add2(k0 < row, k0, tk[0], k8 < row, k8, tk[8]);
                     add2(c9[1] < row, c9[1], tk[1], c9[7] < row, c9[7], tk[7]);
                     s = p9[2] ? s + tk[2] : s;
                     s = p9[3] ? s + tk[3] : s;
@@ -652,7 +654,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                     s = p9[5] ? s + tk[5] : s;
                     s = p9[6] ? s + tk[6] : s;
                     add2(c9[1] > row, c9[1], tk[1], c9[7] > row, c9[7], tk[7]);
-                    add2(c9[0] > row, c9[0], tk[0], c9[8] > row, c9[8], tk[8]);
+                    add2(k0 > row, k0, tk[0], k8 > row, k8, tk[8]);
                     if constexpr (TRIM) {
                         if (p9[3] && ii > 0) sub = sub + d9[3];
                         if (p9[5] && ii < BS - 1) sup = sup + d9[5];
