@@ -180,11 +180,12 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
             assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
             assert np.array_equal(x1, x0), "grid rows change the bits"
             # the split step's SpMV + BJ with x staged through LDS, operands 1..4 groups ahead
-            for wgs, pd in ((1, 3), (3, 1), (4096, 2), (7, 4)):
-                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_pd=pd):
+            # (and 512-row groups)
+            for wgs, pd, gr in ((1, 3, 256), (3, 1, 256), (4096, 2, 256), (7, 4, 256), (1, 1, 512), (5, 1, 512)):
+                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_pd=pd, g4_gr=gr):
                     x3, i3, s3 = _solve(vk_lib, A, M, b, orth=orth)
                 assert i3 == 0 and s3.inner_iters == s1.inner_iters
-                assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs, pd)
+                assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs, pd, gr)
             xd, _, sd = _solve(vk_lib, A, M, b, orth=orth)   # default: the ring split step
             assert sd.inner_iters == s1.inner_iters and np.array_equal(x1, xd)
             # the ring with the step's dots fused in: the dots sum in another fixed order

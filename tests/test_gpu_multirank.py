@@ -40,6 +40,9 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
         if from_host == "planes_ring":   # the LDS-ring step with the dots fused, across ranks
             ctx.set_tuning("g4_ring", 64)
             ctx.set_tuning("g4_dc", 1)
+        elif from_host == "planes_ring512":   # ... and in 512-row groups, dots apart
+            ctx.set_tuning("g4_ring", 2)
+            ctx.set_tuning("g4_gr", 512)
     offs = vk.partition_rows(p.n, world, align)
     rb, re_ = int(offs[rank]), int(offs[rank + 1])
     if from_host == "npz":   # this rank's row block of a SciPy archive (vtkrylov.load_npz)
@@ -75,7 +78,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
                                                        ("C1", 2, False, "dcgs2"), ("C1", 3, False, "dcgs2"),
                                                        ("S2", 2, True, "dcgs2"), ("S2", 4, False, "dcgs2"),
                                                        ("S4", 3, "planes", "dcgs2"), ("S4", 2, "planes_ring", "dcgs2"),
-                                                       ("S4", 3, "planes_ring", "dcgs2"), ("S4F", 2, "planes_ring", "mgs")])
+                                                       ("S4", 3, "planes_ring", "dcgs2"), ("S4F", 2, "planes_ring", "mgs"),
+                                                       ("S4", 2, "planes_ring512", "dcgs2")])
 def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 

@@ -82,7 +82,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
-    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr},
 };
 
 const TuneKey *tune_key(const char *name) {
@@ -1216,7 +1216,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                     solver_matrix_bytes(s.A) + b_inv + 2 * n8 + (dc ? n8 * j : 0.0));   // D, m, x, w (+ V_j)
             int grid = 0;
             HIPCHK(c, launch_g4_ring(s.A->g4, pj, c->dist ? s.A->d_halo : nullptr, s.M->d_tri + s.M->tri_ld, s.w, n,
-                                     s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, dc ? &dd : nullptr,
+                                     s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, dc ? &dd : nullptr,
                                      &grid, stop, j, c->stream));
             if (dc) cnt = grid;
         } else {

@@ -856,14 +856,14 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
 // buffers) and wave wv reads the group's rows of V[k], k = wv, wv + 4, ... (the split of
 // dc_rows); the w write stays (the update pass reads it).
 constexpr int G4TAB = 1024;
-template <typename VT, bool HALO, int RL, int PD, bool DC>
-__global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
+template <typename VT, bool HALO, int RL, int PD, bool DC, int GR>
+__global__ __launch_bounds__(GR) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
                                                 const double *__restrict__ mtri, double *__restrict__ w, int n,
                                                 int ngroups_per_wg, G4Dots dd, const int *stop_col, int col) {
     __shared__ double ring[RL];
     __shared__ double tb[G4TAB];
-    constexpr int KPW = DC_MAXJ / (NT / 64);
-    __shared__ double pw[DC ? 2 : 1][DC ? 2 * NT : 1];
+    constexpr int KPW = DC_MAXJ / (GR / 64);
+    __shared__ double pw[DC ? 2 : 1][DC ? 2 * GR : 1];
     double ds_[KPW], dz_[KPW], daa = 0.0, dab = 0.0, dag = 0.0;
 #pragma unroll
     for (int u = 0; u < KPW; ++u) ds_[u] = dz_[u] = 0.0;
@@ -871,19 +871,19 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
     const int tid = threadIdx.x, lane = tid & 63, ii = lane & 7;
     const int Nvy = g.Nvy, Nvx = g.Nvx, Ny = g.Ny;
     const int S2 = Nvy, S3 = Nvx * Nvy, S4 = Ny * S3;
-    const int ng = (n + 255) / 256;
+    const int ng = (n + (GR - 1)) / GR;
     const int gb = blockIdx.x * ngroups_per_wg, ge = min(ng, gb + ngroups_per_wg);
     if (gb >= ge) return;
     const int oy = 2 * Nvx, ovx = oy + 2 * Nvy, ovy = ovx + 2 * g.X;
     const int lb = g.lblk;
     // the value tables in LDS (a table load in the row loop would be a global load issued after
     // the queue's prefetch: waiting for it would wait for the whole queue)
-    for (int i = tid; i < ovy + 2 * Ny; i += NT) tb[i] = g.tab[i];
-    // the window's initial rows [gb 256 - S3, gb 256 + 256 + S3), clamped to [0, n)
-    for (int r = gb * 256 - S3 + tid; r < gb * 256 + 256 + S3; r += NT)
+    for (int i = tid; i < ovy + 2 * Ny; i += GR) tb[i] = g.tab[i];
+    // the window's initial rows [gb GR - S3, gb GR + GR + S3), clamped to [0, n)
+    for (int r = gb * GR - S3 + tid; r < gb * GR + GR + S3; r += GR)
         if (r >= 0 && r < n) ring[r % RL] = x[r];
-    // 256 in the mixed radix (Nvy, Nvx, Ny, X)
-    const int a0 = 256 % Nvy, q0 = 256 / Nvy, a1 = q0 % Nvx, q1 = q0 / Nvx, a2 = q1 % Ny, a3 = q1 / Ny;
+    // GR in the mixed radix (Nvy, Nvx, Ny, X)
+    const int a0 = GR % Nvy, q0 = GR / Nvy, a1 = q0 % Nvx, q1 = q0 / Nvx, a2 = q1 % Ny, a3 = q1 / Ny;
     struct Co {
         int jvy, jvx, iy, ix;
     };
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
     };
     Co lead;
     {
-        const int r = gb * 256 + tid;
+        const int r = gb * GR + tid;
         lead.jvy = r % Nvy;
         const int t1 = r / Nvy;
         lead.jvx = t1 % Nvx;
@@ -925,9 +925,9 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
         lead.ix = t2 / Ny;
     }
     auto load = [&](int gl, Ld &o) {
-        const int r = gl * 256 + tid;
+        const int r = gl * GR + tid;
         const int rc = min(r, n - 1);
-        o.xn = x[min(r + 256 + S3, n - 1)];
+        o.xn = x[min(r + GR + S3, n - 1)];
         int cm, cp;
         xcols(rc, cm, cp);
         o.xm = xat(cm);
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
     Ld qu[PD];
 #pragma unroll
     for (int k = 0; k < PD; ++k) load(gb + k, qu[k]);
-    int sb = (gb * 256 + tid) % RL;   // ring slot of the lane's row
+    int sb = (gb * GR + tid) % RL;   // ring slot of the lane's row
     auto slot = [&](int off) {
         int t = sb + off;
         t += t < 0 ? RL : 0;
@@ -955,7 +955,7 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
 #pragma unroll
         for (int k = 0; k + 1 < PD; ++k) qu[k] = qu[k + 1];
         load(gi + PD, qu[PD - 1]);
-        const int r = gi * 256 + tid;
+        const int r = gi * GR + tid;
         const bool act = r < n;
         const int rc = act ? r : n - 1;
         const int jvy = cu.c.jvy, jvx = cu.c.jvx, iy = cu.c.iy, ix = cu.c.ix;
@@ -999,27 +999,27 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
         const int buf = gi & 1;
         if constexpr (DC) {
             pw[buf][tid] = act ? x0 : 0.0;
-            pw[buf][NT + tid] = act ? z : 0.0;
+            pw[buf][GR + tid] = act ? z : 0.0;
         }
         // slide the window: the rows of group gi + 1's upper edge (their slots held rows the
         // remaining groups no longer read; the ring is > 2 S3 + 512 long)
-        if (r + 256 + S3 < n) ring[slot(256 + S3)] = cu.xn;
-        sb = slot(256);
+        if (r + GR + S3 < n) ring[slot(GR + S3)] = cu.xn;
+        sb = slot(GR);
         __syncthreads();
         if constexpr (DC) {
             // the group's dots (the other buffer is written next; this one again only after the
             // next barrier, which every wave reaches after these reads)
             const int wv = tid >> 6;
-            const double *pt = pw[buf], *wt = pw[buf] + NT;
+            const double *pt = pw[buf], *wt = pw[buf] + GR;
 #pragma unroll
             for (int u = 0; u < KPW; ++u) {
-                const int k = wv + u * (NT / 64);
+                const int k = wv + u * (GR / 64);
                 if (k < dd.j) {
                     const double *vk = dd.V + (size_t)k * dd.ld;
 #pragma unroll
-                    for (int h = 0; h < NT / 64; ++h) {
+                    for (int h = 0; h < GR / 64; ++h) {
                         const int i = lane + 64 * h;
-                        const double v = __builtin_nontemporal_load(vk + min(gi * 256 + i, n - 1));
+                        const double v = __builtin_nontemporal_load(vk + min(gi * GR + i, n - 1));
                         ds_[u] += v * pt[i];
                         dz_[u] += v * wt[i];
                     }
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
             }
             if (wv == 0) {
 #pragma unroll
-                for (int h = 0; h < NT / 64; ++h) {
+                for (int h = 0; h < GR / 64; ++h) {
                     const int i = lane + 64 * h;
                     daa += pt[i] * pt[i];
                     dab += pt[i] * wt[i];
@@ -1042,14 +1042,14 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
         double *red = ring;
 #pragma unroll
         for (int u = 0; u < KPW; ++u) {
-            const int k = wv + u * (NT / 64);
+            const int k = wv + u * (GR / 64);
             const double ts = wave_sum(ds_[u]), tz = wave_sum(dz_[u]);
             if (lane == 0 && k < dd.j) { red[k] = ts; red[DC_MAXJ + k] = tz; }
         }
         const double t0 = wave_sum(daa), t1 = wave_sum(dab), t2 = wave_sum(dag);
         if (wv == 0 && lane == 0) { red[2 * DC_MAXJ] = t0; red[2 * DC_MAXJ + 1] = t1; red[2 * DC_MAXJ + 2] = t2; }
         __syncthreads();
-        for (int q = tid; q < DC_NQ; q += NT) {
+        for (int q = tid; q < DC_NQ; q += GR) {
             const bool used = q < dd.j || (q >= DC_MAXJ && q < DC_MAXJ + dd.j) || q >= 2 * DC_MAXJ;
             if (used) dd.part[(size_t)q * GMAX + blockIdx.x] = red[q];
         }
@@ -1057,43 +1057,47 @@ __global__ __launch_bounds__(NT) void k_g4_ring(Grid4 g, const double *__restric
 }
 
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
-                          int fp32, int wgs, int pd, int xcd, const G4Dots *dots, int *grid_out, const int *stop_col,
-                          int col, hipStream_t s) {
+                          int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out,
+                          const int *stop_col, int col, hipStream_t s) {
+    // gr: rows per group = lanes per workgroup (256, or 512 without the fused dots)
+    const int G = gr >= 512 && !dots ? 512 : 256;
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy, S4 = S3 * g.Ny;
-    if (!g.tab || !g.D || 2 * S3 + 512 > 8192 || n <= 0 || n > INT32_MAX / 2 || S4 <= 0 || n % S4 ||
-        2 * (g.Nvx + g.Nvy + g.X + g.Ny) > G4TAB ||
-        (halo == nullptr) != (g.lblk < 0))
+    if (!g.tab || !g.D || 2 * S3 + 2 * G > 8192 || n <= 0 || n > INT32_MAX / 2 || S4 <= 0 || n % S4 ||
+        2 * (g.Nvx + g.Nvy + g.X + g.Ny) > G4TAB || (halo == nullptr) != (g.lblk < 0))
         return hipErrorInvalidValue;
-    const bool small = 2 * S3 + 512 <= 4608;
-    const int64_t ng = (n + 255) / 256;
+    // the ring: the window 2 S3 + G plus the next group's rows
+    const bool small = 2 * S3 + 2 * G <= (G == 256 ? 4608 : 5120);
+    const int64_t ng = (n + G - 1) / G;
     int64_t per = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
     // xcd > 0: ranges of S4 / xcd rows, so that the ranges reading a range's rows as their x -+ 1
     // planes are xcd workgroups away -- on the same XCD (workgroups are dealt round-robin over the
     // eight XCDs) when xcd is a multiple of 8: those reads hit that XCD's L2
-    if (xcd > 0) per = std::max<int64_t>(1, (S4 + 128 * xcd) / (256 * (int64_t)xcd));
+    if (xcd > 0) per = std::max<int64_t>(1, (S4 + G / 2 * xcd) / (G * (int64_t)xcd));
     // the fused dots write one partial per workgroup: at most GMAX workgroups
     if (dots) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
-    const dim3 grid((unsigned)((ng + per - 1) / per)), blk(NT);
+    const dim3 grid((unsigned)((ng + per - 1) / per)), blk(G);
     if (dots && (dots->j < 0 || dots->j > DC_MAXJ || !dots->V || !dots->part)) return hipErrorInvalidValue;
     if (grid_out) *grid_out = (int)grid.x;
     const G4Dots dd = dots ? *dots : G4Dots{};
-#define VTK_G4R(VT_, H_, RL_, PD_, DC_) \
-    hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, PD_, DC_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, dd, \
-                       stop_col, col)
-#define VTK_G4R_PD(VT_, H_, RL_) \
+#define VTK_G4R(VT_, H_, RL_, PD_, DC_, GR_) \
+    hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, PD_, DC_, GR_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, \
+                       dd, stop_col, col)
+#define VTK_G4R_PD(VT_, H_) \
     do { \
-        if (dots) VTK_G4R(VT_, H_, RL_, 1, true); \
-        else if (pd <= 1) VTK_G4R(VT_, H_, RL_, 1, false); \
-        else if (pd == 2) VTK_G4R(VT_, H_, RL_, 2, false); \
-        else if (pd == 3) VTK_G4R(VT_, H_, RL_, 3, false); \
-        else VTK_G4R(VT_, H_, RL_, 4, false); \
+        if (G == 512) { if (small) VTK_G4R(VT_, H_, 5120, 1, false, 512); else VTK_G4R(VT_, H_, 8192, 1, false, 512); } \
+        else if (!small) { if (dots) VTK_G4R(VT_, H_, 8192, 1, true, 256); else VTK_G4R(VT_, H_, 8192, 1, false, 256); } \
+        else if (dots) VTK_G4R(VT_, H_, 4608, 1, true, 256); \
+        else if (pd <= 1) VTK_G4R(VT_, H_, 4608, 1, false, 256); \
+        else if (pd == 2) VTK_G4R(VT_, H_, 4608, 2, false, 256); \
+        else if (pd == 3) VTK_G4R(VT_, H_, 4608, 3, false, 256); \
+        else VTK_G4R(VT_, H_, 4608, 4, false, 256); \
     } while (0)
     if (fp32) {
-        if (halo) { if (small) VTK_G4R_PD(float, true, 4608); else VTK_G4R_PD(float, true, 8192); }
-        else { if (small) VTK_G4R_PD(float, false, 4608); else VTK_G4R_PD(float, false, 8192); }
+        if (halo) VTK_G4R_PD(float, true);
+        else VTK_G4R_PD(float, false);
     } else {
-        if (halo) { if (small) VTK_G4R_PD(double, true, 4608); else VTK_G4R_PD(double, true, 8192); }
-        else { if (small) VTK_G4R_PD(double, false, 4608); else VTK_G4R_PD(double, false, 8192); }
+        if (halo) VTK_G4R_PD(double, true);
+        else VTK_G4R_PD(double, false);
     }
 #undef VTK_G4R_PD
 #undef VTK_G4R

@@ -173,6 +173,7 @@ struct Tuning {
     int g4_pd = 1;            // k_g4_ring: groups of operands loaded ahead (1..4)
     int g4_xcd = 0;           // k_g4_ring: > 0: ranges of S4 / g4_xcd rows (overrides g4_ring's count)
     int g4_dc = 0;            // k_g4_ring: the DCGS2 step's dots fused in
+    int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
 };
 }  // namespace vtk
 
@@ -529,7 +530,7 @@ struct G4Dots {
     double *part = nullptr;
 };
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
-                          int fp32, int wgs, int pd, int xcd, const G4Dots *dots, int *grid_out, const int *stop_col,
+                          int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
                           int col, hipStream_t s);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
