@@ -30,9 +30,9 @@ import statistics
 CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv3 output (default
               # path: SELL-64 layout, tridiagonal-factor BJ(8), DCGS2; fp64 or fp32 values)
     "band_step": r"void vtk::k_band_step<",
-    "spmv_bj_dc": r"void vtk::k_(sell<(double|float), false, 4, 8, true,|g4_ring<(double|float), false, \d+, \d+, true>)",
+    "spmv_bj_dc": r"void vtk::k_(sell<(double|float), false, 4, 8, true,|g4_ring<(double|float), false, \d+, \d+, true(, \d+)?>)",
     "spmv": r"void vtk::k_sell<(double|float), false, 0, 1, false,",
-    "spmv_bj": r"void vtk::k_(sell<(double|float), false, 2, 8, true,|g4_ring<(double|float), false, \d+, \d+, false>)",
+    "spmv_bj": r"void vtk::k_(sell<(double|float), false, 2, 8, true,|g4_ring<(double|float), false, \d+, \d+, false(, \d+)?>)",
     "spmv_resid_bj": r"void vtk::k_sell<(double|float), false, 3, 8, true,",
     "spmv_csr": r"void vtk::k_spmv<(double|float), false, 0, 1",
     "spmv_bj_dc_csr": r"void vtk::k_spmv<(double|float), false, 4, 8",
