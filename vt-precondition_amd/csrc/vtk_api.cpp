@@ -82,7 +82,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
-    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr}, {"upd_grid", &Tuning::upd_grid}, {"upd_xb", &Tuning::upd_xb},
 };
 
 const TuneKey *tune_key(const char *name) {
@@ -1307,8 +1307,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             HIPCHK(c, launch_line_sweep(a, s.sweep_R, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
-            HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1,
-                                       c->stream));
+            HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, c->tune.upd_grid > 0 ? c->tune.upd_grid : s.G, ds,
+                                       s.x, s.H, s.S, m, fused ? 0 : 1, c->tune.upd_xb, c->stream));
         }
         // throttle: an event every EV_EVERY steps (each record costs the stream a few us); the
         // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
@@ -1598,7 +1598,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         // x += y @ V[:col+1] (:799-814), r = b - A x, rnorm (:816-817)
         const size_t xup_idx = c->prof_pending.size();
         { Prof pf(c, "xupdate", -1, 0.0);   // bytes set once the stop column is known
-          HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream)); }
+          HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->tune.upd_xb, c->stream)); }
         TRY(residual());
         HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -397,10 +397,12 @@ __device__ inline void hess_solve(const double *__restrict__ H, const double *__
 // c = stop_col is j-1 (column j-1 finalised in step j: V[0..j-1] all stored) or j (column j
 // committed early: v_j = (p_j - V_j s) / r formed here exactly as the normal pass would store
 // it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
-static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
-                                        const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
-                                        const double *__restrict__ S, int m, const double *__restrict__ wprev,
-                                        const double *__restrict__ pj_at = nullptr) {
+template <int XB>
+static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict__ V, int64_t ld, int j, int c,
+                                                       int64_t n, const DcCoef *cf, double *__restrict__ x,
+                                                       const double *__restrict__ H, const double *__restrict__ S,
+                                                       int m, const double *__restrict__ wprev,
+                                                       const double *__restrict__ pj_at = nullptr) {
     __shared__ double ys[DC_MAXJ + 1], cs[DC_MAXJ], ep[DC_MAXJ];
     __shared__ double rinv_s, qp_s;
     // wprev (line-band step): p_j is not stored; recompute it as step j-1 formed it
@@ -425,10 +427,24 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
         if (i + 1 < n) {
             double ax = 0.0, ay = 0.0;
             double2 a = make_double2(0.0, 0.0);
+            // XB > 1: the basis rows in batches of XB loads issued together; the sums in ascending
+            // k either way
             if (rec) {
                 const d2v wp = ldnt2(wprev + i);
                 double tx = wp.x, ty = wp.y;
-                for (int k = 0; k < j; ++k) {
+                int k = 0;
+                if constexpr (XB > 1)
+                for (; k + XB <= j; k += XB) {
+                    d2v v[XB];
+#pragma unroll
+                    for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
+#pragma unroll
+                    for (int u = 0; u < XB; ++u) {
+                        tx = tx - ep[k + u] * v[u].x;
+                        ty = ty - ep[k + u] * v[u].y;
+                    }
+                }
+                for (; k < j; ++k) {
                     const d2v v = ldnt2(V + (size_t)k * ld + i);
                     tx = tx - ep[k] * v.x;
                     ty = ty - ep[k] * v.y;
@@ -438,8 +454,7 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
                 const d2v pp = ldnt2(pj + i);
                 a = make_double2(pp.x, pp.y);
             }
-            for (int k = 0; k < kv; ++k) {
-                const d2v v = ldnt2(V + (size_t)k * ld + i);
+            auto acc1 = [&](int k, const d2v &v) {
                 ax += ys[k] * v.x;
                 ay += ys[k] * v.y;
                 if (c == j) {
@@ -447,7 +462,17 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
                     a.x = a.x - sk * v.x;
                     a.y = a.y - sk * v.y;
                 }
+            };
+            int k = 0;
+            if constexpr (XB > 1)
+            for (; k + XB <= kv; k += XB) {
+                d2v v[XB];
+#pragma unroll
+                for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
+#pragma unroll
+                for (int u = 0; u < XB; ++u) acc1(k + u, v[u]);
             }
+            for (; k < kv; ++k) acc1(k, ldnt2(V + (size_t)k * ld + i));
             if (c == j) {
                 const double vx = j >= 1 ? a.x * rinv : a.x, vy = j >= 1 ? a.y * rinv : a.y;
                 ax += ys[j] * vx;
@@ -473,6 +498,15 @@ static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int
             x[i] = x[i] + ax;
         }
     }
+}
+
+// the band-step kernels call the x update out of line (their register allocation stays their own);
+// k_dc_update inlines dc_xupdate_body (global, not flat, loads)
+[[maybe_unused]] static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
+                                        const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
+                                        const double *__restrict__ S, int m, const double *__restrict__ wprev,
+                                        const double *__restrict__ pj_at = nullptr) {
+    dc_xupdate_body<1>(V, ld, j, c, n, cf, x, H, S, m, wprev, pj_at);
 }
 
 }  // namespace vtk

@@ -174,6 +174,8 @@ struct Tuning {
     int g4_xcd = 0;           // k_g4_ring: > 0: ranges of S4 / g4_xcd rows (overrides g4_ring's count)
     int g4_dc = 0;            // k_g4_ring: the DCGS2 step's dots fused in
     int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
+    int upd_grid = 0;         // k_dc_update workgroups (0: the dots grid)
+    int upd_xb = 0;           // k_dc_update, k_xupdate: basis rows loaded in batches of 8 (A/B: neutral)
 };
 }  // namespace vtk
 
@@ -385,7 +387,7 @@ hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresSt
 // y = triangular solve (H, S) at stop column; x += y @ V
 // (returns at entry when a DCGS2 update pass already did it: st->xup_tag >= 0)
 hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld,
-                          double *x, int64_t n, int m, const GmresState *st, int grid,
+                          double *x, int64_t n, int m, const GmresState *st, int grid, int xb,
                           hipStream_t s);
 // dst = sqrt(reduce(p)) if do_sqrt else reduce(p)   (single workgroup)
 hipError_t launch_finalize(Red p, double *dst, int do_sqrt, hipStream_t s);
@@ -427,7 +429,7 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 // c = j the v_j of the pass is formed in registers), reading the basis once
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
                             const DcCoef *cf, int grid, const GmresState *st, double *x,
-                            const double *H, const double *S, int m, int nt_pw, hipStream_t s);
+                            const double *H, const double *S, int m, int nt_pw, int xb, hipStream_t s);
 
 // Line-band DCGS2 step (k_band_step): update pass of step j + SpMV, tridiagonal
 // BJ(8) and dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded

@@ -2229,6 +2229,7 @@ hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresSt
 // (iterative.py:799-814).  Workgroup-redundant triangular solve on lane 0, into LDS.
 // ------------------------------------------------------------------------------------------
 
+template <int XB>
 __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, const double *__restrict__ S,
                                                 const double *__restrict__ V, int64_t ld,
                                                 double *__restrict__ x, int64_t n, int m,
@@ -2242,7 +2243,19 @@ __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, co
     for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
         if (i + 1 < n) {
             double ax = 0.0, ay = 0.0;
-            for (int k = 0; k <= col; ++k) {
+            int k = 0;   // XB > 1: basis rows loaded in batches (sums in ascending k)
+            if constexpr (XB > 1)
+            for (; k + XB <= col + 1; k += XB) {
+                d2v v[XB];
+#pragma unroll
+                for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
+#pragma unroll
+                for (int u = 0; u < XB; ++u) {
+                    ax += ys[k + u] * v[u].x;
+                    ay += ys[k + u] * v[u].y;
+                }
+            }
+            for (; k <= col; ++k) {
                 const d2v v = ldnt2(V + (size_t)k * ld + i);
                 ax += ys[k] * v.x;
                 ay += ys[k] * v.y;
@@ -2260,9 +2273,9 @@ __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, co
 }
 
 hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld, double *x,
-                          int64_t n, int m, const GmresState *st, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_xupdate, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n,
-                       m, st);
+                          int64_t n, int m, const GmresState *st, int grid, int xb, hipStream_t s) {
+    if (xb > 0) hipLaunchKernelGGL(k_xupdate<8>, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n, m, st);
+    else hipLaunchKernelGGL(k_xupdate<0>, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n, m, st);
     return hipGetLastError();
 }
 
@@ -2623,7 +2636,8 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 
 // NTPW: p_j and w loaded non-temporal (A/B: +2 % on the unfused (line) path, -1 % after the
 // fused BJ step, whose w the update re-reads warm)
-template <bool NTPW>
+// XB > 0: the basis rows loaded in batches of XB (the same sums in the same order)
+template <bool NTPW, int XB>
 __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_t ld, int j,
                                                   const double *__restrict__ w, int64_t n,
                                                   const DcCoef *cf, const GmresState *st, double *x,
@@ -2631,7 +2645,7 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
     __shared__ double cs[DC_MAXJ], ce[DC_MAXJ + 1];
     __shared__ double rinv_s, q_s;
     if (VTK_XUP_FUSED && __builtin_nontemporal_load(&st->xup_tag) == j) {
-        dc_xupdate(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m, nullptr);
+        dc_xupdate_body<XB>(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m, nullptr);
         return;
     }
     if (stopped(&st->stop_col, j)) return;
@@ -2657,14 +2671,24 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
                 t = *reinterpret_cast<const double2 *>(w + i);
             }
             double2 a = p;
-            for (int k = 0; k < j; ++k) {
-                const d2v v = ldnt2(V + (size_t)k * ld + i);
+            auto acc1 = [&](int k, const d2v &v) {
                 const double sk = cs[k], ek = ce[k];
                 a.x = a.x - sk * v.x;
                 a.y = a.y - sk * v.y;
                 t.x = t.x - ek * v.x;
                 t.y = t.y - ek * v.y;
+            };
+            int k = 0;
+            if constexpr (XB > 0) {
+                for (; k + XB <= j; k += XB) {
+                    d2v v[XB];
+#pragma unroll
+                    for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
+#pragma unroll
+                    for (int u = 0; u < XB; ++u) acc1(k + u, v[u]);
+                }
             }
+            for (; k < j; ++k) acc1(k, ldnt2(V + (size_t)k * ld + i));
             double2 vj = p;
             if (j >= 1) {
                 vj.x = a.x * rinv;
@@ -2696,12 +2720,17 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
 
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n, const DcCoef *cf,
                             int grid, const GmresState *st, double *x, const double *H, const double *S, int m,
-                            int nt_pw, hipStream_t s) {
+                            int nt_pw, int xb, hipStream_t s) {
 #ifdef VTK_UPD_NTPW_FORCE
     nt_pw = VTK_UPD_NTPW_FORCE;
 #endif
-    if (nt_pw) hipLaunchKernelGGL(k_dc_update<true>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
-    else hipLaunchKernelGGL(k_dc_update<false>, dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+    if (xb > 0) {
+        if (nt_pw) hipLaunchKernelGGL((k_dc_update<true, 8>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+        else hipLaunchKernelGGL((k_dc_update<false, 8>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+    } else {
+        if (nt_pw) hipLaunchKernelGGL((k_dc_update<true, 0>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+        else hipLaunchKernelGGL((k_dc_update<false, 0>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+    }
     return hipGetLastError();
 }
 
