@@ -177,15 +177,18 @@ def test_band_line_separable_values_bit_identical(vk_lib, gpu, name):
     assert A.line_separable and A.line_values == 2   # the Vlasov rows are canonical too
     M = vk_lib.block_jacobi(A, 8)
     b = twin.rhs(p.n)
-    x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
-    with gpu.tuning(band_lsv=0):
+    # (cyc_ring 0: the cycle-start launches through k_sell, which sums its reductions in the same
+    # order with and without the tables; the ring form is pinned by test_cycle_ring_epilogues)
+    with gpu.tuning(cyc_ring=0):
+        x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+    with gpu.tuning(band_lsv=0, cyc_ring=0):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     # canonical rows (the kinds' order from the row's line instead of the SELL codes) vs the codes
-    with gpu.tuning(band_canon=0):
+    with gpu.tuning(band_canon=0, cyc_ring=0):
         x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     # the cycle-start SELL launches (residual + BJ, step 0's SpMV + BJ + dots) with their columns
     # from canon_row vs the codes
-    with gpu.tuning(sell_canon=0):
+    with gpu.tuning(sell_canon=0, cyc_ring=0):
         x3, i3, s3 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     assert s1.band == s0.band == s2.band == s3.band == 1 and i1 == i0 == i2 == i3 == 0
     assert s1.inner_iters == s0.inner_iters == s2.inner_iters == s3.inner_iters
@@ -231,14 +234,40 @@ def test_separable_values_in_unfused_paths_bit_identical(vk_lib, gpu, orth):
     assert A.line_separable
     M = vk_lib.block_jacobi(A, 8)
     b = twin.rhs(p.n)
-    x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
-    with gpu.tuning(band_lsv=0):
+    with gpu.tuning(cyc_ring=0):
+        x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
+    with gpu.tuning(band_lsv=0, cyc_ring=0):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
-    with gpu.tuning(sell_canon=0):   # the SELL codes instead of canon_row's columns
+    with gpu.tuning(sell_canon=0, cyc_ring=0):   # the SELL codes instead of canon_row's columns
         x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, False, orth=orth)
     assert s1.band == s0.band == s2.band == 0 and i1 == i0 == i2 == 0
     assert s1.inner_iters == s0.inner_iters == s2.inner_iters
     assert np.array_equal(x1, x0)
     assert np.array_equal(x1, x2)
+    M.close()
+    A.close()
+
+
+@pytest.mark.parametrize("name,band,orth", [("S2", True, "dcgs2"), ("C1", True, "dcgs2"), ("C1", False, "mgs")])
+def test_cycle_ring_epilogues(vk_lib, gpu, name, band, orth):
+    """The cycle-start residual + BJ and the band cycle's step 0 through the x-line ring
+    (k_lsv_ring_epi, tuning cyc_ring): the same row sums and BJ solves as k_sell's
+    canonical rows, the norms and dots reduced in another fixed order -- within the solver bars
+    of the k_sell form, bit-identical from run to run, for any workgroup count; several cycles
+    (restart 5) and x0 != 0 so that every cycle starts with the ring residual."""
+    p, A = _op(vk_lib, gpu, name)
+    M = vk_lib.block_jacobi(A, 8)
+    b = twin.rhs(p.n)
+    x0 = twin.rhs(p.n, seed=0xB0B) * 1e-3
+    with gpu.tuning(cyc_ring=0):
+        xr, ir, sr = _solve(vk_lib, gpu, A, M, b, band, restart=5, orth=orth, x0=x0)
+    for wgs in (1, 64, 1024):
+        with gpu.tuning(cyc_ring=wgs):
+            xa, ia, sa = _solve(vk_lib, gpu, A, M, b, band, restart=5, orth=orth, x0=x0)
+            xb, ib, sb = _solve(vk_lib, gpu, A, M, b, band, restart=5, orth=orth, x0=x0)
+        assert ia == ib == ir == 0 and sa.band == sr.band == int(band)
+        assert np.array_equal(xa, xb) and sa.inner_iters == sb.inner_iters, wgs
+        assert abs(sa.inner_iters - sr.inner_iters) <= 1, wgs
+        assert np.linalg.norm(xa - xr) / np.linalg.norm(xr) < 1e-9, wgs
     M.close()
     A.close()

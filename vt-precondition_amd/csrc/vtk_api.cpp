@@ -82,7 +82,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
-    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr}, {"upd_grid", &Tuning::upd_grid}, {"upd_xb", &Tuning::upd_xb},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr}, {"upd_grid", &Tuning::upd_grid}, {"cyc_ring", &Tuning::cyc_ring}, {"upd_xb", &Tuning::upd_xb},
 };
 
 const TuneKey *tune_key(const char *name) {
@@ -1028,6 +1028,16 @@ struct Solver {
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
+// the x-line ring with the solver's epilogues (k_lsv_ring_epi): one rank, line-separable canonical
+// rows, their tables in use (tunings band_lsv, sell_canon), the tridiagonal BJ(8) when bj
+bool cyc_ring_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M, bool bj) {
+    if (c->tune.cyc_ring <= 0 || c->dist || !A->d_lsv || !A->lsv_canon || A->band_L <= 0 || A->band_L % 8 != 0 ||
+        !c->tune.band_lsv || !c->tune.sell_canon || band_parts(A->band_L) < 1 || A->n_local / A->band_L < 3)
+        return false;
+    if (!bj) return true;
+    return M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr;
+}
+
 int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0,
                    bool want_dots = true) {
     vtk_ctx *c = s.c;
@@ -1178,6 +1188,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                          c->stream));
                 cnt += spmv_grid(bd);
             }
+        } else if (fused && band && j == 0 && cyc_ring_ok(c, s.A, s.M, true)) {
+            // step 0 of a band cycle through the x-line ring (x = v_0; the j = 0 dots only)
+            Prof pf(c, "spmv_bj_dc", j, b_step);
+            HIPCHK(c, launch_lsv_ring_epi(EPI_PREC_DC, s.A->d_lsv, pj, nullptr, s.M->d_tri + s.M->tri_ld, s.w, nullptr,
+                                          nullptr, s.dcpart, n, (int)s.A->band_L, c->tune.cyc_ring, stop, j, &cnt,
+                                          c->stream));
         } else if (fused) {
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
@@ -1490,13 +1506,29 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         TRY(halo_exchange(A, x));
         int rc2;
         Red rr;
-        if (fres) {
+        if (fres && M && cyc_ring_ok(c, A, M, true)) {   // the same through the x-line ring
+            Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
+            int g = 0;
+            HIPCHK(c, launch_lsv_ring_epi(EPI_RESID_PREC, A->d_lsv, x, b, M->d_tri + M->tri_ld, s.V, prr, prz, nullptr,
+                                          n, (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream));
+            rr = reduce(c, prr, g, rc2);
+            TRY(rc2);
+            rz = reduce(c, prz, g, rc2);
+            TRY(rc2);
+        } else if (fres) {
             Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
             HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, rtiles, x), A), EPI_RESID_PREC, s.V, b, bj_op(M),
                                   nullptr, prr, prz, nullptr, 0, c->stream));
             rr = reduce(c, prr, spmv_grid(rin0), rc2);
             TRY(rc2);
             rz = reduce(c, prz, spmv_grid(rin0), rc2);
+            TRY(rc2);
+        } else if (cyc_ring_ok(c, A, M, false)) {
+            Prof pf(c, "spmv_resid", -1, solver_matrix_bytes(A) + 3 * n8);
+            int g = 0;
+            HIPCHK(c, launch_lsv_ring_epi(EPI_RESID, A->d_lsv, x, b, nullptr, s.r, prr, nullptr, nullptr, n,
+                                          (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream));
+            rr = reduce(c, prr, g, rc2);
             TRY(rc2);
         } else {
             Prof pf(c, "spmv_resid", -1, solver_matrix_bytes(A) + 3 * n8);

@@ -1246,6 +1246,157 @@ hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s) {
     return hipGetLastError();
 }
 
+// k_lsv_ring with the solver's epilogues (one rank, canonical rows): the row sum
+// exactly as k_lsv_ring / k_sell's canonical rows, then
+//   EPI_RESID       r = b - A x -> y, |r|^2                         (cycle start, line path)
+//   EPI_RESID_PREC  r = b - A x, z = M^-1 r -> y, |r|^2, |z|^2      (cycle start, BJ(8))
+//   EPI_PREC_DC     z = M^-1 A x -> y, |x|^2, x.z, |z|^2            (DCGS2 step 0, BJ(8))
+// with M^-1 the tridiagonal BJ(8) of bj_trim_group (the same operations as k_sell's TRIM
+// epilogue).  The reductions: per lane over its rows in line order, then wave_sum, then the
+// waves in order -- one partial per workgroup (PREC_DC: launch_dc_dots' layout).
+struct LsvEpiK {
+    const double *lsv, *x, *b, *mtri;
+    double *y, *p0, *p1, *dcpart;
+    int n, L, H;
+    const int *stop_col;
+    int col;
+};
+template <int EPI>
+__global__ __launch_bounds__(BAND_T) void k_lsv_ring_epi(LsvEpiK a) {
+    __shared__ double ring[4 * BAND_T];
+    __shared__ double red[3][BAND_T / 64];
+    if (stopped(a.stop_col, a.col)) return;
+    const double *__restrict__ lsv = a.lsv;
+    const double *__restrict__ x = a.x;
+    const int n = a.n, L = a.L, H = a.H;
+    const int tid = threadIdx.x, lane = tid & 63, ii = lane & 7, X = n / L, LP = L / H;
+    const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
+    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R), nl = xb - xa;
+    const int v = v0 - 8 + tid;
+    const bool inl = v >= 0 && v < L && tid < LP + 16;
+    const bool own = tid >= 8 && tid < 8 + LP;
+    const double tx0 = own ? lsv[n + v] : 0.0, tx1 = own ? lsv[n + L + v] : 0.0;
+    auto line_of = [&](int it) { return it == 0 ? (xa == 0 ? X - 1 : xa - 1) : (it == nl + 1 ? (xb == X ? 0 : xb) : xa - 1 + it); };
+    auto slot = [&](int it) { return (it & 3) * BAND_T; };
+    constexpr bool BJ = EPI == EPI_RESID_PREC || EPI == EPI_PREC_DC;
+    constexpr bool HB = EPI == EPI_RESID || EPI == EPI_RESID_PREC;
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+    // prefetch: x of line_of(it), and D (m, b) of line it - 1 (computed at iteration it)
+    double nxv = inl ? __builtin_nontemporal_load(x + (int64_t)line_of(0) * L + v) : 0.0, nd = 0.0, nm = 1.0, nb = 0.0;
+    for (int it = 0; it <= nl + 1; ++it) {
+        ring[slot(it) + tid] = nxv;
+        const double drow = nd, mrow = nm, brow = nb;
+        if (it <= nl) {
+            nxv = inl ? __builtin_nontemporal_load(x + (int64_t)line_of(it + 1) * L + v) : 0.0;
+            if (own && it + 1 >= 2) {
+                const int64_t rr = (int64_t)(xa + it - 1) * L + v;
+                nd = __builtin_nontemporal_load(lsv + rr);
+                if constexpr (BJ) nm = __builtin_nontemporal_load(a.mtri + rr);
+                if constexpr (HB) nb = __builtin_nontemporal_load(a.b + rr);
+            }
+        }
+        __syncthreads();
+        if (it >= 2) {
+            const int xl = xa + it - 2;
+            const double tv0 = lsv[n + 2 * L + xl], tv1 = lsv[n + 2 * L + X + xl];
+            int64_t cxm, cxp;
+            const int ord = __builtin_amdgcn_readfirstlane(canon_order_xv(xl, 0, n, L, X, -1, cxm, cxp));
+            constexpr int P_MID = 0 | 1 << 3 | 2 << 6 | 3 << 9 | 4 << 12;
+            constexpr int P_FIRST = 1 | 2 << 3 | 3 << 6 | 4 << 9 | 0 << 12;
+            const int sx = slot(it - 1);
+            const double t0 = tx0 * ring[slot(it - 2) + tid];
+            const double t4 = tx1 * ring[slot(it) + tid];
+            const double xr = ring[sx + tid];
+            const double t2 = drow * xr;
+            const double t1 = tv0 * ring[sx + tid - (tid > 0 ? 1 : 0)];
+            const double t3 = tv1 * ring[sx + tid + (tid < BAND_T - 1 ? 1 : 0)];
+            const bool h1 = v > 0, h3 = v < L - 1;
+            double sa = 0.0;
+            if (ord == P_MID) {
+                sa = sa + t0;
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+                sa = sa + t4;
+            } else if (ord == P_FIRST) {
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+                sa = sa + t4;
+                sa = sa + t0;
+            } else {
+                sa = sa + t4;
+                sa = sa + t0;
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+            }
+            const int64_t row = (int64_t)xl * L + v;
+            double out = sa;
+            if constexpr (HB) {
+                out = own ? brow - sa : 0.0;   // r = b - A x
+                acc0 += out * out;
+            }
+            if constexpr (BJ) {
+                const double sub = (own && h1 && ii > 0) ? 0.0 + tv0 : 0.0;
+                const double sup = (own && h3 && ii < 7) ? 0.0 + tv1 : 0.0;
+                const double z = bj_trim_group<8>(own ? out : 0.0, lane, sub, sup, own ? mrow : 1.0);
+                if constexpr (EPI == EPI_RESID_PREC) {
+                    if (own) acc1 += z * z;
+                } else {
+                    if (own) {
+                        acc0 += xr * xr;
+                        acc1 += xr * z;
+                        acc2 += z * z;
+                    }
+                }
+                out = z;
+            }
+            if (own) __builtin_nontemporal_store(out, a.y + row);
+        }
+    }
+    const int wid = tid >> 6;
+    const double t0 = wave_sum(acc0), t1 = wave_sum(acc1), t2 = wave_sum(acc2);
+    if (lane == 0) {
+        red[0][wid] = t0;
+        red[1][wid] = t1;
+        red[2][wid] = t2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+        double sum = 0.0;
+#pragma unroll
+        for (int w = 0; w < BAND_T / 64; ++w) sum += red[tid][w];
+        if constexpr (EPI == EPI_PREC_DC) a.dcpart[(size_t)(2 * DC_MAXJ + tid) * GMAX + b] = sum;
+        else if (tid == 0) a.p0[b] = sum;
+        else if (tid == 1 && EPI == EPI_RESID_PREC) a.p1[b] = sum;
+    }
+}
+
+hipError_t launch_lsv_ring_epi(int epi, const double *lsv, const double *x, const double *b, const double *mtri,
+                               double *y, double *p0, double *p1, double *dcpart, int64_t n, int L, int ring_wgs,
+                               const int *stop_col, int col, int *grid_out, hipStream_t s) {
+    const int H = band_parts(L);
+    const int64_t X = L > 0 ? n / L : 0;
+    if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || H < 1 || X < 3 || ring_wgs < 1) return hipErrorInvalidValue;
+    const bool bj = epi == EPI_RESID_PREC || epi == EPI_PREC_DC;
+    if ((bj && !mtri) || ((epi == EPI_RESID || epi == EPI_RESID_PREC) && (!b || !p0)) ||
+        (epi == EPI_RESID_PREC && !p1) || (epi == EPI_PREC_DC && !dcpart) || L % 8 != 0)
+        return hipErrorInvalidValue;
+    // one partial per workgroup: at most GMAX
+    const int64_t R = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ring_wgs / H, X / 2), GMAX / H));
+    LsvEpiK a{lsv, x, b, mtri, y, p0, p1, dcpart, (int)n, L, H, stop_col, col};
+    const dim3 g((unsigned)(R * H)), blk(BAND_T);
+    if (grid_out) *grid_out = (int)g.x;
+    switch (epi) {
+        case EPI_RESID: hipLaunchKernelGGL(k_lsv_ring_epi<EPI_RESID>, g, blk, 0, s, a); break;
+        case EPI_RESID_PREC: hipLaunchKernelGGL(k_lsv_ring_epi<EPI_RESID_PREC>, g, blk, 0, s, a); break;
+        case EPI_PREC_DC: hipLaunchKernelGGL(k_lsv_ring_epi<EPI_PREC_DC>, g, blk, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
                            hipStream_t s, int canon, int grid_cap, int ring_wgs) {

@@ -175,6 +175,8 @@ struct Tuning {
     int g4_dc = 0;            // k_g4_ring: the DCGS2 step's dots fused in
     int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
     int upd_grid = 0;         // k_dc_update workgroups (0: the dots grid)
+    int cyc_ring = 512;       // > 0: cycle-start residual and DCGS2 step 0 through the x-line ring
+                              // (k_lsv_ring_epi, ~that many workgroups; 2D line-separable, one rank)
     int upd_xb = 0;           // k_dc_update, k_xupdate: basis rows loaded in batches of 8 (A/B: neutral)
 };
 }  // namespace vtk
@@ -489,6 +491,13 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
                             int lblk, double *lsv, int *bad, hipStream_t s);
 // y = A x from the line-separable tables and the SELL codes (uniform width 5, coded columns):
 // k_sell's plain SpMV, the same bits.  halo != null: the distributed layout (lblk the left block)
+// the x-line ring SpMV with the solver's epilogues (one rank, canonical rows; k_lsv_ring_epi):
+// EPI_RESID (y = b - A x, p0 = |r|^2 partials), EPI_RESID_PREC (y = M^-1 (b - A x), p0, p1 =
+// |r|^2, |z|^2), EPI_PREC_DC (y = M^-1 A x, DCGS2 step-0 dots |x|^2, x.y, |y|^2 into dcpart);
+// *grid_out partials (<= GMAX)
+hipError_t launch_lsv_ring_epi(int epi, const double *lsv, const double *x, const double *b, const double *mtri,
+                               double *y, double *p0, double *p1, double *dcpart, int64_t n, int L, int ring_wgs,
+                               const int *stop_col, int col, int *grid_out, hipStream_t s);
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
                            hipStream_t s, int canon, int grid_cap,
