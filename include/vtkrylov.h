@@ -172,7 +172,7 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
  * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_canon_sl, sell_pad,
  * sell_grid, plain_grid, sell_swz, plain_var, band_opt, band_j3, lsv_spmv_cap, lsv_ring,
  * line_sweep, ev_every, prof_perj, debug_band, comm_solo, auto_band, grid4, c4_fused, g4_ring,
- * g4_pd, g4_xcd, g4_dc, g4_gr, upd_grid, upd_xb, cyc_ring.
+ * g4_pd, g4_xcd, g4_dc, g4_gr, upd_grid, upd_xb, cyc_ring, g4_dc0, g4_res.
  * VTK_ERR_ARG for an unknown key.  (ABI 5) */
 int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);
 int vtk_ctx_get_tuning(vtk_ctx *ctx, const char *key, int *value);

@@ -182,14 +182,20 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
             # the split step's SpMV + BJ with x staged through LDS, operands 1..4 groups ahead
             # (and 512-row groups)
             for wgs, pd, gr in ((1, 3, 256), (3, 1, 256), (4096, 2, 256), (7, 4, 256), (1, 1, 512), (5, 1, 512)):
-                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_pd=pd, g4_gr=gr):
+                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_pd=pd, g4_gr=gr, g4_dc0=0, g4_res=0):
                     x3, i3, s3 = _solve(vk_lib, A, M, b, orth=orth)
                 assert i3 == 0 and s3.inner_iters == s1.inner_iters
                 assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs, pd, gr)
-            xd, _, sd = _solve(vk_lib, A, M, b, orth=orth)   # default: the ring split step
-            assert sd.inner_iters == s1.inner_iters and np.array_equal(x1, xd)
+            # default: the ring split step, step 0's dots and the cycle-start residual in the ring
+            # kernel (reductions in another fixed order: the solver bars; deterministic)
+            xd, _, sd = _solve(vk_lib, A, M, b, orth=orth)
+            xe, _, se = _solve(vk_lib, A, M, b, orth=orth, x0=b * 1e-3)
+            xf, _, sf = _solve(vk_lib, A, M, b, orth=orth, x0=b * 1e-3)
+            assert np.array_equal(xe, xf) and se.inner_iters == sf.inner_iters
+            assert abs(sd.inner_iters - s1.inner_iters) <= 1
+            assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) < 1e-9
             # the ring with the step's dots fused in: the dots sum in another fixed order
-            with gpu.tuning(g4_ring=2048, g4_dc=1):
+            with gpu.tuning(g4_ring=2048, g4_dc=1, g4_res=0):
                 x4, i4, s4 = _solve(vk_lib, A, M, b, orth=orth)
                 x5, _, _ = _solve(vk_lib, A, M, b, orth=orth)
             assert i4 == 0 and np.array_equal(x4, x5)

@@ -82,7 +82,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
     {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
     {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
-    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr}, {"upd_grid", &Tuning::upd_grid}, {"cyc_ring", &Tuning::cyc_ring}, {"upd_xb", &Tuning::upd_xb},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr}, {"upd_grid", &Tuning::upd_grid}, {"cyc_ring", &Tuning::cyc_ring}, {"g4_dc0", &Tuning::g4_dc0}, {"g4_res", &Tuning::g4_res}, {"upd_xb", &Tuning::upd_xb},
 };
 
 const TuneKey *tune_key(const char *name) {
@@ -1038,6 +1038,12 @@ bool cyc_ring_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M, bool bj) {
     return M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr;
 }
 
+// the 4D grid rows' cycle-start residual through k_g4_ring (tunings g4_ring, g4_res; BJ(8) tridiag)
+bool g4_resid_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M) {
+    return A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && c->tune.g4_res && A->use_sell &&
+           A->sell.uniform_w > 8 && M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr;
+}
+
 int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0,
                    bool want_dots = true) {
     vtk_ctx *c = s.c;
@@ -1227,7 +1233,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             dd.ld = s.ld;
             dd.j = j;
             dd.part = s.dcpart;
-            const bool dc = c->tune.g4_dc != 0;
+            // g4_dc: every step's dots fused in; step 0's (|p|^2, p.w, |w|^2 only) by default
+            const bool dc = c->tune.g4_dc != 0 || (j == 0 && c->tune.g4_dc0 != 0);
+            dd.mode = c->tune.g4_dc != 0 ? 1 : 2;
             Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j,
                     solver_matrix_bytes(s.A) + b_inv + 2 * n8 + (dc ? n8 * j : 0.0));   // D, m, x, w (+ V_j)
             int grid = 0;
@@ -1506,7 +1514,22 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         TRY(halo_exchange(A, x));
         int rc2;
         Red rr;
-        if (fres && M && cyc_ring_ok(c, A, M, true)) {   // the same through the x-line ring
+        if (fres && M && g4_resid_ok(c, A, M)) {   // 4D grid rows: through k_g4_ring
+            Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
+            G4Dots dd;
+            dd.mode = 3;
+            dd.b = b;
+            dd.p0 = prr;
+            dd.p1 = prz;
+            int g = 0;
+            HIPCHK(c, launch_g4_ring(A->g4, x, c->dist ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
+                                     c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, &dd, &g, nullptr,
+                                     0, c->stream));
+            rr = reduce(c, prr, g, rc2);
+            TRY(rc2);
+            rz = reduce(c, prz, g, rc2);
+            TRY(rc2);
+        } else if (fres && M && cyc_ring_ok(c, A, M, true)) {   // the same through the x-line ring
             Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
             int g = 0;
             HIPCHK(c, launch_lsv_ring_epi(EPI_RESID_PREC, A->d_lsv, x, b, M->d_tri + M->tri_ld, s.V, prr, prz, nullptr,

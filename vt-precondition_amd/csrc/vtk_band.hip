@@ -855,16 +855,23 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
 // workgroup in launch_dc_dots' partial layout.  Each group's p and w are staged in LDS (two
 // buffers) and wave wv reads the group's rows of V[k], k = wv, wv + 4, ... (the split of
 // dc_rows); the w write stays (the update pass reads it).
+// MODE (G4Dots::mode): 0 w = M^-1 A x; 1 DC (the dots above); 2 DCGS2 step 0 (j = 0: |p|^2,
+// p.w, |w|^2, each lane over its own rows); 3 the cycle-start residual r = b - A x, w = M^-1 r,
+// |r|^2, |w|^2 (partials p0, p1) -- k_sell<EPI_RESID_PREC>'s operations.  Modes 1-3: one partial
+// per workgroup, lanes -> waves -> workgroup in a fixed order.
 constexpr int G4TAB = 1024;
-template <typename VT, bool HALO, int RL, int PD, bool DC, int GR>
-__global__ __launch_bounds__(GR) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
+template <typename VT, bool HALO, int RL, int PD, int MODE, int GR>
+__global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 && RL <= 5120 && MODE != 1 ? 6 : 1))) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
                                                 const double *__restrict__ mtri, double *__restrict__ w, int n,
                                                 int ngroups_per_wg, G4Dots dd, const int *stop_col, int col) {
+    constexpr bool DC = MODE == 1, RES = MODE == 3;
     __shared__ double ring[RL];
     __shared__ double tb[G4TAB];
+    __shared__ double red3[3][MODE >= 2 ? GR / 64 : 1];
     constexpr int KPW = DC_MAXJ / (GR / 64);
     __shared__ double pw[DC ? 2 : 1][DC ? 2 * GR : 1];
     double ds_[KPW], dz_[KPW], daa = 0.0, dab = 0.0, dag = 0.0;
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;   // MODE 2 / 3: the lane's sums over its rows
 #pragma unroll
     for (int u = 0; u < KPW; ++u) ds_[u] = dz_[u] = 0.0;
     if (stopped(stop_col, col)) return;
@@ -911,7 +918,7 @@ __global__ __launch_bounds__(GR) void k_g4_ring(Grid4 g, const double *__restric
     };
     auto xat = [&](int c) { return HALO ? *(c >= n ? halo + (c - n) : x + c) : x[c]; };
     struct Ld {
-        double xn, xm, xp, xw, m, d;
+        double xn, xm, xp, xw, m, d, b;
         Co c;
     };
     Co lead;
@@ -936,6 +943,7 @@ __global__ __launch_bounds__(GR) void k_g4_ring(Grid4 g, const double *__restric
         o.xw = x[min(max(cw, 0), n - 1)];
         o.m = __builtin_nontemporal_load(mtri + rc);
         o.d = (double)__builtin_nontemporal_load(static_cast<const VT *>(g.D) + rc);
+        o.b = RES ? __builtin_nontemporal_load(dd.b + rc) : 0.0;
         o.c = lead;
         adv(lead);
     };
@@ -994,8 +1002,22 @@ __global__ __launch_bounds__(GR) void k_g4_ring(Grid4 g, const double *__restric
         add2(cym > rc, cym, t1y, cyp > rc, cyp, t7);
         add2(km > rc, km, t0, kp > rc, kp, t8);
         const double sub = (pym && ii > 0) ? 0.0 + d3 : 0.0, sup = (pyp && ii < 7) ? 0.0 + d5 : 0.0;
-        const double z = bj_trim_group<8>(act ? s : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
+        double sv = s;
+        if constexpr (RES) {   // r = b - A x (iterative.py:816)
+            sv = act ? cu.b - s : 0.0;
+            e0 += sv * sv;
+        }
+        const double z = bj_trim_group<8>(act ? sv : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
         if (act) __builtin_nontemporal_store(z, w + r);
+        if constexpr (RES) {
+            if (act) e1 += z * z;
+        } else if constexpr (MODE == 2) {
+            if (act) {
+                e0 += x0 * x0;
+                e1 += x0 * z;
+                e2 += z * z;
+            }
+        }
         const int buf = gi & 1;
         if constexpr (DC) {
             pw[buf][tid] = act ? x0 : 0.0;
@@ -1054,13 +1076,32 @@ __global__ __launch_bounds__(GR) void k_g4_ring(Grid4 g, const double *__restric
             if (used) dd.part[(size_t)q * GMAX + blockIdx.x] = red[q];
         }
     }
+    if constexpr (MODE >= 2) {
+        const int wid = tid >> 6;
+        const double t0 = wave_sum(e0), t1 = wave_sum(e1), t2 = wave_sum(e2);
+        if (lane == 0) {
+            red3[0][wid] = t0;
+            red3[1][wid] = t1;
+            red3[2][wid] = t2;
+        }
+        __syncthreads();
+        if (tid < 3) {
+            double sum = 0.0;
+#pragma unroll
+            for (int wv = 0; wv < GR / 64; ++wv) sum += red3[tid][wv];
+            if constexpr (MODE == 2) dd.part[(size_t)(2 * DC_MAXJ + tid) * GMAX + blockIdx.x] = sum;
+            else if (tid == 0) dd.p0[blockIdx.x] = sum;
+            else if (tid == 1) dd.p1[blockIdx.x] = sum;
+        }
+    }
 }
 
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
                           int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out,
                           const int *stop_col, int col, hipStream_t s) {
-    // gr: rows per group = lanes per workgroup (256, or 512 without the fused dots)
-    const int G = gr >= 512 && !dots ? 512 : 256;
+    // gr: rows per group = lanes per workgroup (256, or 512 without the fused dots of mode 1)
+    const int mode = dots ? dots->mode : 0;
+    const int G = gr >= 512 && mode != 1 ? 512 : 256;
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy, S4 = S3 * g.Ny;
     if (!g.tab || !g.D || 2 * S3 + 2 * G > 8192 || n <= 0 || n > INT32_MAX / 2 || S4 <= 0 || n % S4 ||
         2 * (g.Nvx + g.Nvy + g.X + g.Ny) > G4TAB || (halo == nullptr) != (g.lblk < 0))
@@ -1073,24 +1114,33 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
     // planes are xcd workgroups away -- on the same XCD (workgroups are dealt round-robin over the
     // eight XCDs) when xcd is a multiple of 8: those reads hit that XCD's L2
     if (xcd > 0) per = std::max<int64_t>(1, (S4 + G / 2 * xcd) / (G * (int64_t)xcd));
-    // the fused dots write one partial per workgroup: at most GMAX workgroups
-    if (dots) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
+    // the fused reductions write one partial per workgroup: at most GMAX workgroups
+    if (mode) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
     const dim3 grid((unsigned)((ng + per - 1) / per)), blk(G);
-    if (dots && (dots->j < 0 || dots->j > DC_MAXJ || !dots->V || !dots->part)) return hipErrorInvalidValue;
+    if (mode < 0 || mode > 3 || (mode == 1 && (dots->j < 0 || dots->j > DC_MAXJ || !dots->V || !dots->part)) ||
+        (mode == 2 && !dots->part) || (mode == 3 && (!dots->b || !dots->p0 || !dots->p1)))
+        return hipErrorInvalidValue;
     if (grid_out) *grid_out = (int)grid.x;
     const G4Dots dd = dots ? *dots : G4Dots{};
 #define VTK_G4R(VT_, H_, RL_, PD_, DC_, GR_) \
     hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, PD_, DC_, GR_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, \
                        dd, stop_col, col)
+#define VTK_G4R_M(VT_, H_, RL_, GR_) \
+    do { \
+        if (mode == 1) VTK_G4R(VT_, H_, RL_, 1, 1, GR_); \
+        else if (mode == 2) VTK_G4R(VT_, H_, RL_, 1, 2, GR_); \
+        else if (mode == 3) VTK_G4R(VT_, H_, RL_, 1, 3, GR_); \
+        else VTK_G4R(VT_, H_, RL_, 1, 0, GR_); \
+    } while (0)
 #define VTK_G4R_PD(VT_, H_) \
     do { \
-        if (G == 512) { if (small) VTK_G4R(VT_, H_, 5120, 1, false, 512); else VTK_G4R(VT_, H_, 8192, 1, false, 512); } \
-        else if (!small) { if (dots) VTK_G4R(VT_, H_, 8192, 1, true, 256); else VTK_G4R(VT_, H_, 8192, 1, false, 256); } \
-        else if (dots) VTK_G4R(VT_, H_, 4608, 1, true, 256); \
-        else if (pd <= 1) VTK_G4R(VT_, H_, 4608, 1, false, 256); \
-        else if (pd == 2) VTK_G4R(VT_, H_, 4608, 2, false, 256); \
-        else if (pd == 3) VTK_G4R(VT_, H_, 4608, 3, false, 256); \
-        else VTK_G4R(VT_, H_, 4608, 4, false, 256); \
+        if (G == 512) { if (small) VTK_G4R_M(VT_, H_, 5120, 512); else VTK_G4R_M(VT_, H_, 8192, 512); } \
+        else if (!small) VTK_G4R_M(VT_, H_, 8192, 256); \
+        else if (mode) VTK_G4R_M(VT_, H_, 4608, 256); \
+        else if (pd <= 1) VTK_G4R(VT_, H_, 4608, 1, 0, 256); \
+        else if (pd == 2) VTK_G4R(VT_, H_, 4608, 2, 0, 256); \
+        else if (pd == 3) VTK_G4R(VT_, H_, 4608, 3, 0, 256); \
+        else VTK_G4R(VT_, H_, 4608, 4, 0, 256); \
     } while (0)
     if (fp32) {
         if (halo) VTK_G4R_PD(float, true);
@@ -1100,6 +1150,7 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
         else VTK_G4R_PD(double, false);
     }
 #undef VTK_G4R_PD
+#undef VTK_G4R_M
 #undef VTK_G4R
     return hipGetLastError();
 }

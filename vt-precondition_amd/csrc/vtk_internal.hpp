@@ -173,6 +173,8 @@ struct Tuning {
     int g4_pd = 1;            // k_g4_ring: groups of operands loaded ahead (1..4)
     int g4_xcd = 0;           // k_g4_ring: > 0: ranges of S4 / g4_xcd rows (overrides g4_ring's count)
     int g4_dc = 0;            // k_g4_ring: the DCGS2 step's dots fused in
+    int g4_dc0 = 1;           // k_g4_ring: step 0's dots (|p|^2, p.w, |w|^2) fused in
+    int g4_res = 1;           // k_g4_ring: the cycle-start residual + BJ (r = b - A x) too
     int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
     int upd_grid = 0;         // k_dc_update workgroups (0: the dots grid)
     int cyc_ring = 512;       // > 0: cycle-start residual and DCGS2 step 0 through the x-line ring
@@ -532,13 +534,17 @@ hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s);
 // w = M^-1 A x for 4D grid rows with x staged through LDS (k_g4_ring): the tridiagonal BJ(8) of
 // m = mtri; about wgs workgroups, each a contiguous range of 256-row groups; halo != null: across
 // ranks (g.lblk the left plane's halo block).  Bit-identical to the SELL launch.  dots != null:
-// DCGS2 step dots->j fused in (x = V[j]), partials per workgroup (launch_dc_dots' layout; at most
-// GMAX workgroups, the count in *grid_out).
+// DCGS2 step dots->j fused in (x = V[j], mode 1; mode 2 the j = 0 dots alone) or the cycle-start
+// residual (mode 3, w = M^-1 (b - A x)); partials per workgroup (at most GMAX workgroups, the
+// count in *grid_out).
 struct G4Dots {
+    int mode = 1;                  // 1: step j's dots; 2: step 0's dots; 3: cycle-start residual
     const double *V = nullptr;
     int64_t ld = 0;
     int j = 0;
-    double *part = nullptr;
+    double *part = nullptr;        // modes 1, 2: the dots partials (launch_dc_dots' layout)
+    const double *b = nullptr;     // mode 3: the right-hand side; |r|^2, |w|^2 partials
+    double *p0 = nullptr, *p1 = nullptr;
 };
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
                           int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
