@@ -52,6 +52,10 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 #ifndef VTK_BAND_REREAD
 #define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
 #endif
+#ifndef VTK_BAND_XUP_INLINE
+#define VTK_BAND_XUP_INLINE 4   // > 0: the cycle's x update inlined into k_band_step, basis loads in batches of
+                                // this many (0: the out-of-line call; C3 xupdate 648-653 -> 641-643 us)
+#endif
 #ifndef VTK_BAND_PF
 #define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 10)   // j <= this: next line's update operands prefetched across SpMV + dots
                                                  // (10: 567-570 us; 8: 570; 12: 567; 18: 624, spills)
@@ -90,7 +94,11 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     __shared__ double cs[BAND_JV], ce[BAND_JV], cp[BAND_JV];
     constexpr int j = J;
     if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
-        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, a.w_prev);
+        if constexpr (VTK_BAND_XUP_INLINE > 0)
+            dc_xupdate_body<VTK_BAND_XUP_INLINE>(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf,
+                                                 a.x, a.H, a.S, a.m, a.w_prev);
+        else
+            dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, a.w_prev);
         return;
     }
     if (stopped(&a.st->stop_col, j)) return;
