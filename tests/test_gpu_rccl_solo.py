@@ -53,3 +53,24 @@ def test_rccl_solo_gmres(vk_lib, solo, layout, orth):
         # and no boundary rows, so no exchange and no boundary launch
         assert "dc_finalize" in prof and "spmv_bj_dc" in prof
         assert "spmv_bj_dc_bd" not in prof and "halo" not in prof
+
+
+@pytest.mark.parametrize("name", ["S4", "S4F"])
+def test_rccl_solo_grid4(vk_lib, solo, name):
+    """The 4D grid rows on the one-rank RCCL communicator: no neighbour planes, so the one-rank
+    (periodic) form of the grid and of k_g4_ring runs inside the distributed code paths, x0 != 0
+    so that the cycles start with the ring residual."""
+    vk = vk_lib
+    p = twin.CONFIGS[name]
+    A = vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=solo)
+    assert A.grid4 == tuple(p.shape[1:])
+    ip, ix, d = coracle.generate(p)
+    M = vk.block_jacobi(A, 8)
+    b = twin.rhs(p.n)
+    x0 = twin.rhs(p.n, seed=0xB0B) * 1e-3
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), x0=x0, rtol=1e-8, restart=5)
+    xs, info = vk.gmres(A, b, x0=x0, rtol=1e-8, M=M, restart=5)
+    st = vk.last_stats()
+    assert info == ref.info == 0
+    assert abs(st.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(xs - ref.x) / np.linalg.norm(ref.x) <= 1e-9

@@ -1239,7 +1239,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j,
                     solver_matrix_bytes(s.A) + b_inv + 2 * n8 + (dc ? n8 * j : 0.0));   // D, m, x, w (+ V_j)
             int grid = 0;
-            HIPCHK(c, launch_g4_ring(s.A->g4, pj, c->dist ? s.A->d_halo : nullptr, s.M->d_tri + s.M->tri_ld, s.w, n,
+            HIPCHK(c, launch_g4_ring(s.A->g4, pj, s.A->g4.lblk >= 0 ? s.A->d_halo : nullptr, s.M->d_tri + s.M->tri_ld, s.w, n,
                                      s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, dc ? &dd : nullptr,
                                      &grid, stop, j, c->stream));
             if (dc) cnt = grid;
@@ -1522,7 +1522,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             dd.p0 = prr;
             dd.p1 = prz;
             int g = 0;
-            HIPCHK(c, launch_g4_ring(A->g4, x, c->dist ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
+            HIPCHK(c, launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
                                      c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, &dd, &g, nullptr,
                                      0, c->stream));
             rr = reduce(c, prr, g, rc2);
