@@ -149,7 +149,9 @@ struct Tuning {
     int sell_pad = 1;         // pad nearly uniform SELL widths (<= 2 % more entries)
     int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
     int plain_grid = 2048;    // workgroups of the plain SELL SpMV
-    int sell_swz = 0;         // SELL launches walk their groups in XCD-contiguous order
+    int sell_swz = 1;         // SELL launches walk their groups in XCD-contiguous order: bit 0 the
+                              // plain SpMV (vtk_spmv; C3 PMC 1.40 -> 1.07 GB per launch, time
+                              // neutral), bit 1 the other epilogues (their partials follow the order)
     int plain_var = 1;        // plain SELL SpMV variant bits (k_sell VAR: 1 = padding gathers branched;
                               // in-process A/B C3: 243.6 -> 221.3 us, the round-1 kernel's 218-222 us)
     int band_opt = 3;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B

@@ -1141,7 +1141,8 @@ template <typename VT, bool HALO>
 static hipError_t spmv_dispatch(const SpmvIn &in, int epi, double *y, const double *b, const BjOp &bj,
                                 const double *v0, double *part0, double *part1, const int *stop_col, int col,
                                 hipStream_t s) {
-    const SpmvK<VT, HALO> a = spmv_args<VT, HALO>(in, y, b, bj, v0, part0, part1, stop_col, col);
+    SpmvK<VT, HALO> a = spmv_args<VT, HALO>(in, y, b, bj, v0, part0, part1, stop_col, col);
+    a.swz = (in.swz >> (epi == EPI_PLAIN ? 0 : 1)) & 1;   // Tuning::sell_swz
     const bool sell = in.sell && in.groups;
     const dim3 g(spmv_grid(in)), blk(NT);
     const int bs = (bj.inv || bj.tri) ? bj.bs : 0;
@@ -1169,6 +1170,7 @@ template <typename VT, bool HALO>
 static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, const double *V, int64_t ld,
                                    int j, double *part, const int *stop_col, int col, hipStream_t s) {
     SpmvK<VT, HALO> a = spmv_args<VT, HALO>(in, w, nullptr, bj, nullptr, nullptr, nullptr, stop_col, col);
+    a.swz = (in.swz >> 1) & 1;   // Tuning::sell_swz bit 1 (the partials follow the group order)
     a.V = V;
     a.ld = ld;
     a.j = j;
