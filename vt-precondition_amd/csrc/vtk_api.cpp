@@ -341,7 +341,9 @@ SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nu
         in.groups = g ? g : &A->g_all;
     }
     in.plain_grid = A->ctx->tune.plain_grid;
-    in.swz = A->ctx->tune.sell_swz;
+    // (the 9-wide 4D rows' plain SpMV: 648 -> 730 us swizzled -- their x +- 1 planes are 250 000
+    // rows away, not in the XCD's window -- so blockIdx order there)
+    in.swz = A->ctx->tune.sell_swz & ((A->use_sell && A->sell.uniform_w > 8) ? ~1 : ~0);
     in.plain_var = A->ctx->tune.plain_var;
     return in;
 }
