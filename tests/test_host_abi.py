@@ -230,3 +230,17 @@ def test_line_band_plan_rejects(vk_lib, n, L):
     st, _ = _band_plan(vk_lib, n, L)
     assert st == vk_lib._abi.ERR_ARG
     assert vk_lib._abi.last_error()
+
+
+def test_header_lists_every_tuning_key():
+    """include/vtkrylov.h documents the tuning keys vtk_ctx_set_tuning accepts: the list there is
+    the library's table (vtk_api.cpp TUNE_KEYS), no more and no fewer."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "vtkrylov.h")).read()
+    m = re.search(r"Keys:(.*?)\.\s*\n\s*\* VTK_ERR_ARG for an unknown key", hdr, re.S)
+    assert m, "key list not found in the header"
+    listed = {k.strip() for k in m.group(1).replace("*", " ").replace("\n", " ").split(",")}
+    src = open(os.path.join(root, "vt-precondition_amd", "csrc", "vtk_api.cpp")).read()
+    table = set(re.findall(r'\{"([a-z0-9_]+)", &Tuning::', src))
+    assert listed == table, (sorted(listed - table), sorted(table - listed))
