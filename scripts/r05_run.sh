@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-5 GPU steps: each stage under its own time limit, stop at the first failure.
+#   STAGES="band ab" scripts/r05_run.sh      (AB_ENV / AB_VALUES / AB_SET / AB_CFG pick the A/B)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() { local name=$1 to=$2; shift 2; echo "== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; grep -v "^Extension\|amdgpu.ids\|^W20\|^E20\|^I20" "gpurun_out/$name.log" | tail -n 3 | cut -c1-800; [ $rc -le 1 ] || { echo "!! $name rc=$rc"; exit $rc; }; [ $rc -eq 0 ] || { echo "!! $name failed"; exit 1; }; }
+T="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread"
+for st in ${STAGES:-band}; do case $st in
+band) run t_band 600 $T tests/test_gpu_band.py ;;
+tests) run t_sel 900 $T ${TESTS} ;;
+gpu) run t_gpu 1100 $T tests -m gpu ;;
+smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+ab) run ab_${AB_ENV} 600 python tools/ab_env.py --env "$AB_ENV" --values "${AB_VALUES:-1,0}" --rounds "${AB_ROUNDS:-4}" --config "${AB_CFG:-C3}" --set "${AB_SET:-}" --perj ;;
+bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+*) echo "unknown stage $st"; exit 2 ;;
+esac; done

@@ -238,3 +238,23 @@ def test_grid4_rejects_other_structures(vk_lib, gpu):
     assert C2.grid4 == (0, 0, 0) and C2.line_band == S2.shape[1]
     for o in (A, B, C2):
         o.close()
+
+
+@pytest.mark.parametrize("shape", [(520, 3, 4, 4), (3, 3, 64, 64)])
+def test_grid4_past_ring_limits(vk_lib, gpu, shape):
+    """4D grids past k_g4_ring's LDS limits -- the coordinate tables over 1024 doubles
+    (520 x planes on one rank) or the y-line window over the ring (Nvx Nvy = 4096) -- solve
+    through the SELL grid-row kernels instead of failing in the ring launch."""
+    p = twin.Vlasov(4, shape)
+    G = vk_lib.vlasov_operator(vk_lib.vlasov_params(4, shape), ctx=gpu)
+    assert G.grid4 == tuple(shape[1:])
+    ip, ix, d = G.download()
+    M = vk_lib.block_jacobi(G, 8)
+    b = twin.rhs(p.n)
+    x, info, st = _solve(vk_lib, G, M, b)
+    ref = coracle.gmres(ip, ix, d, b, coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    assert info == ref.info == 0
+    assert abs(st.inner_iters - ref.inner_iters) <= 1
+    assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) < 1e-9
+    M.close()
+    G.close()

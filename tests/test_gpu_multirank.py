@@ -6,6 +6,7 @@ Checks against the single-rank oracle:
   * each rank's SpMV rows and BJ blocks: bit-identical (halo columns keep the row order);
   * the distributed GMRES: same info, inner iterations +-1, ||x - x_ref|| / ||x_ref|| <= 1e-9.
 """
+import json
 import os
 import socket
 
@@ -40,10 +41,14 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
         if from_host == "planes_ring":   # the LDS-ring step with the dots fused, across ranks
             ctx.set_tuning("g4_ring", 64)
             ctx.set_tuning("g4_dc", 1)
-        elif from_host == "planes_ring512":   # ... and in 512-row groups, dots apart
+        elif from_host.startswith("planes_ring512"):   # ... and in 512-row groups, dots apart
             ctx.set_tuning("g4_ring", 2)
             ctx.set_tuning("g4_gr", 512)
+        else:                            # the SELL grid-row split step (interior / boundary groups)
+            ctx.set_tuning("g4_ring", 0)
     offs = vk.partition_rows(p.n, world, align)
+    if from_host == "planes_ring512_uneven":   # slabs of 2 and 4 planes: rank-dependent ring grids
+        offs = np.array([0, 2 * align, p.n], dtype=np.int64)
     rb, re_ = int(offs[rank]), int(offs[rank + 1])
     if from_host == "npz":   # this rank's row block of a SciPy archive (vtkrylov.load_npz)
         A = vk.load_npz(os.path.join(outdir, "A.npz"), ctx=ctx, offsets=offs)
@@ -61,13 +66,17 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
     M = vk.block_jacobi(A, 8)
     inv = M.inverse()
     b = twin.rhs(p.n)
+    ctx.profile(True)
     xs, info = vk.gmres(A, b[rb:re_], rtol=1e-8, M=M, orth=orth)
     st = vk.last_stats()
+    classes = sorted(k for k, e in ctx.profile_read().items() if e["launches"] > 0)
+    ctx.profile(False)
     gip, gix, gd = A.download()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), y=y, inv=inv, x=xs, info=info,
              iters=st.inner_iters, rb=rb, re=re_, halo=A.n_halo, gip=gip, gix=gix, gd=gd, band=st.band,
              line_band=A.line_band,
-             errors=np.array(hc.errors, dtype=object).astype(str))
+             errors=np.array(hc.errors, dtype=object).astype(str), classes=json.dumps(classes),
+             commlog=json.dumps(hc.log))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -79,7 +88,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
                                                        ("S2", 2, True, "dcgs2"), ("S2", 4, False, "dcgs2"),
                                                        ("S4", 3, "planes", "dcgs2"), ("S4", 2, "planes_ring", "dcgs2"),
                                                        ("S4", 3, "planes_ring", "dcgs2"), ("S4F", 2, "planes_ring", "mgs"),
-                                                       ("S4", 2, "planes_ring512", "dcgs2")])
+                                                       ("S4", 2, "planes_ring512", "dcgs2"),
+                                                       ("S4", 2, "planes_ring512_uneven", "dcgs2"), ("S4", 2, "planes", "dcgs2")])
 def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     import torch.multiprocessing as mp
 
@@ -114,3 +124,17 @@ def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
         xs[rb:re_] = z["x"]
     rel = np.linalg.norm(xs - ref.x) / np.linalg.norm(ref.x)
     assert rel <= 1e-9, rel
+    # the step kernel that ran: the 4D ring across ranks books its boundary
+    # planes as spmv_bj_bd, the SELL split step as spmv_bj_dc_bd
+    for r in range(world):
+        cls = set(json.loads(str(np.load(tmp_path / f"rank{r}.npz", allow_pickle=False)["classes"])))
+        if orth != "dcgs2":   # (MGS: SciPy's sequence, precond_matvec's launches)
+            continue
+        if isinstance(from_host, str) and from_host.startswith("planes_ring"):
+            assert "spmv_bj_bd" in cls and "spmv_bj_dc_bd" not in cls, sorted(cls)
+        elif from_host == "planes":
+            assert "spmv_bj_dc_bd" in cls and "spmv_bj_bd" not in cls, sorted(cls)
+    # every rank issued the communicator sequence RCCL could run
+    from vtkrylov.comm import check_sequences
+    check_sequences([json.loads(str(np.load(tmp_path / f"rank{r}.npz", allow_pickle=False)["commlog"]))
+                     for r in range(world)])

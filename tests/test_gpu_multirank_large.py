@@ -15,6 +15,7 @@ within 1e-8 of max|x| (1e-6 when the counts differ by one), and the true residua
 assembled x recomputed on the host by the oracle's SpMV <= rtol ||b||.  C3 also asserts that
 the band step ran across the ranks (stats.band, halo = the two neighbour lines).
 """
+import json
 import os
 import socket
 
@@ -54,7 +55,7 @@ def _worker(rank, world, port, case, outdir):
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), info=info, iters=st.inner_iters, band=st.band,
              rb=rb, re=re_, halo=A.n_halo, line_band=A.line_band, mode=M.mode, layout=A.layout_info()["layout"],
              separable=A.line_separable,
-             errors=np.array(hc.errors, dtype=object).astype(str))
+             errors=np.array(hc.errors, dtype=object).astype(str), commlog=json.dumps(hc.log))
     M.close()
     A.close()
     dist.barrier()
@@ -86,6 +87,13 @@ def test_row_partitioned_full_size(tmp_path, golden_large, case, world):
         iters.append(int(z["iters"]))
         x[rb:re_] = np.load(tmp_path / f"x{r}.npy", allow_pickle=False)
     assert len(set(iters)) == 1, iters          # every rank ran the same Arnoldi steps
+    # the communicator sequence the RCCL transport would issue -- the same
+    # collectives in the same order on every rank, every send matched by the peer's receive
+    from vtkrylov.comm import check_sequences
+    logs = [json.loads(str(np.load(tmp_path / f"rank{r}.npz", allow_pickle=False)["commlog"])) for r in range(world)]
+    nops = check_sequences(logs)
+    kinds = {op[0] for op in logs[0]}
+    assert nops > 2 * it and "allreduce" in kinds and "alltoallv" in kinds, (nops, kinds)
     assert g["source"].startswith("scipy.sparse.linalg.gmres")
     it = iters[0]
     assert abs(it - g["inner_iters"]) <= 1, (it, g["inner_iters"])

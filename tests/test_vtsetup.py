@@ -136,3 +136,86 @@ def test_line_len_node(tmp_path):
     assert SolverConfig.load(str(x)).line_len == 800
     x.write_text(s.replace("<line_len>800</line_len>", ""))
     assert SolverConfig.load(str(x)).line_len is None
+
+
+def test_run_gpus_node(tmp_path):
+    """run/gpus and run/comm: absent -> one rank over RCCL; the nodes are typed and checked."""
+    import shutil
+    c = SolverConfig.load()
+    assert (c.gpus, c.comm) == (1, "rccl")
+    assert SolverConfig.load(gpus=4, comm="host").gpus == 4
+    x = tmp_path / "c.xml"
+    shutil.copy(DEFAULT_XML, x)
+    s = x.read_text()
+    x.write_text(s.replace("<gpus>1</gpus>", "<gpus>8</gpus>"))
+    assert SolverConfig.load(str(x)).gpus == 8
+    x.write_text(s.replace("<gpus>1</gpus>", "").replace("<comm>rccl</comm>", ""))
+    assert (SolverConfig.load(str(x)).gpus, SolverConfig.load(str(x)).comm) == (1, "rccl")
+    with pytest.raises(ValueError):
+        SolverConfig.load(gpus=0)
+    with pytest.raises(ValueError):
+        SolverConfig.load(comm="mpi")
+    assert SolverConfig.load(config="C1").slab_align() == 800
+    assert SolverConfig.load(config="C4").slab_align() == 125 * 50 * 40
+
+
+@pytest.mark.parametrize("name,gpus", [("C1", 2), ("C3", 8), ("C4", 8)])
+def test_main_spawns_ranks_dry_run(name, gpus):
+    """gpus > 1: test_main starts one process per rank before any GPU call (the launcher of
+    bench.py); each rank joins the gloo group and takes an x-slab row block of whole lines /
+    planes.  --dry-run stops there (no GPU), so this runs on the CPU."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "vt-precondition_amd")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([pkg, root]))
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, "-m", "vtsetup.krylov_precondition", "--config", name,
+                          "--gpus", str(gpus), "--comm", "host", "--dry-run"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    ranks = res["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(gpus)) and all(r["world"] == gpus for r in ranks)
+    c = SolverConfig.load(config=name)
+    n = int(np.prod(c.shape))
+    offs = ranks[0]["offsets"]
+    assert offs[0] == 0 and offs[-1] == n and all(r["offsets"] == offs for r in ranks)
+    assert all(o % c.slab_align() == 0 for o in offs)
+    sizes = np.diff(offs)
+    assert sizes.min() > 0 and sizes.max() - sizes.min() <= c.slab_align()
+    assert [tuple(r["rows"]) for r in ranks] == [(offs[q], offs[q + 1]) for q in range(gpus)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["S2", "C1"])
+def test_main_two_ranks_matches_one(gpu, tmp_path, name):
+    """run/gpus = 2 through test_main -- two rank processes (host-staged
+    transport: both on the box's one GPU), x-slab row blocks, the band step across ranks --
+    against the single-rank step: same info, inner iterations within one, x within the DCGS2
+    bars; the report carries the max-over-ranks solve time."""
+    import os
+    import subprocess
+    import sys
+    from vtsetup.krylov_precondition import KrylovPrecondition
+    cfg = SolverConfig.load(config=name, report=str(tmp_path / "r1.json"))
+    step = KrylovPrecondition(cfg, ctx=gpu)
+    r1 = step.main()
+    x1 = np.asarray(step.x)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "vt-precondition_amd")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([pkg, root]))
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, "-m", "vtsetup.krylov_precondition", "--config", name, "--gpus", "2",
+                          "--comm", "host", "--report", str(tmp_path / "r2.json"), "--x-out", str(tmp_path / "x2.npy")],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r2 = json.load(open(tmp_path / "r2.json"))
+    x2 = np.load(tmp_path / "x2.npy")
+    assert r2["ranks"] == 2 and r2["comm"] == "host" and sum(r2["operator"]["rows_per_rank"]) == r1["operator"]["n"]
+    assert r2["solve"]["info"] == r1["solve"]["info"] == 0
+    assert abs(r2["solve"]["inner_iters"] - r1["solve"]["inner_iters"]) <= 1
+    assert r2["solve"]["band_step"] == r1["solve"]["band_step"]
+    assert x2.shape == x1.shape
+    assert np.max(np.abs(x2 - x1)) <= 1e-8 * np.max(np.abs(x1))

@@ -854,8 +854,11 @@ int line_len_candidate(vtk_csr *A, int64_t &L) {
     vtk_ctx *c = A->ctx;
     const int64_t n = A->n_local, N = A->n_global;
     L = 0;
-    std::vector<int64_t> d[2];
-    if (n >= 1) {
+    // the local candidate; a HIP failure here votes "no candidate" (-1) instead of returning, so
+    // that every rank still joins the allgather below
+    auto local = [&]() -> int {
+        std::vector<int64_t> d[2];
+        if (n < 1) return VTK_OK;
         HIPCHK(c, hipStreamSynchronize(c->stream));
         for (int s = 0; s < 2; ++s) {
             const int64_t r = s == 0 ? 0 : n - 1;
@@ -872,22 +875,31 @@ int line_len_candidate(vtk_csr *A, int64_t &L) {
         }
         for (int64_t v : d[0])
             if (std::binary_search(d[1].begin(), d[1].end(), v)) { L = v; break; }
-    }
+        return VTK_OK;
+    };
+    const int lrc = local();
+    if (lrc != VTK_OK) L = -1;
     if (c->dist) {
+        // the context's scalar scratch (no allocation that could fail on one rank only) for up to
+        // 120 ranks
         const int W = c->world;
-        DBuf mine, all;
-        TRY(dalloc(c, mine, sizeof(int64_t)));
-        TRY(dalloc(c, all, (size_t)W * sizeof(int64_t)));
-        HIPCHK(c, hipMemcpyAsync(mine.p, &L, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-        TRY(comm_allgather_i64(c, mine.as<int64_t>(), all.as<int64_t>(), 1));
+        DBuf own;
+        int64_t *mine = reinterpret_cast<int64_t *>(c->d_scal + 128);
+        if (W > 120) {
+            if (dalloc(c, own, (size_t)(W + 1) * sizeof(int64_t)) != VTK_OK) return fail(c, VTK_ERR_NOMEM, "line band detection: allgather buffer");
+            mine = own.as<int64_t>();
+        }
+        HIPCHK(c, hipMemcpyAsync(mine, &L, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+        TRY(comm_allgather_i64(c, mine, mine + 1, 1));
         std::vector<int64_t> h((size_t)W);
-        HIPCHK(c, hipMemcpyAsync(h.data(), all.p, W * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(h.data(), mine + 1, W * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         for (int64_t v : h)
             if (v != h[0]) { L = 0; break; }
         if (L != 0) L = h[0];
     }
-    return VTK_OK;
+    if (L < 0) L = 0;
+    return lrc;
 }
 
 // 4D grid structure (vtk::Grid4): tables built and every entry checked on the device; rank-local
@@ -974,7 +986,10 @@ int auto_grid4(vtk_csr *A) {
     TRY(grid4_candidate(A, Ny, Nvx, Nvy));
     if (Ny <= 0) return VTK_OK;
     const int rc = grid4_set(A, Ny, Nvx, Nvy);
-    return rc == VTK_ERR_ARG ? VTK_OK : rc;
+    // no such grid, or no memory for its tables: the operator keeps the SELL path (the detection is
+    // a speed-up the drop-in CSR does not need)
+    if (rc == VTK_ERR_NOMEM) A->ctx->err.clear();
+    return rc == VTK_ERR_ARG || rc == VTK_ERR_NOMEM ? VTK_OK : rc;
 }
 
 // the drop-in path's line-band detection: the same check vtk_csr_set_line_band runs, on the
@@ -984,8 +999,9 @@ int auto_line_band(vtk_csr *A) {
     int64_t L = 0;
     TRY(line_len_candidate(A, L));
     if (L <= 0) return VTK_OK;   // uniform across ranks: nobody enters the collective below
-    const int rc = band_check_all(A, L);
+    const int rc = band_check_all(A, L);   // collective: every rank gets here (L agreed above)
     if (rc == VTK_OK) A->band_L = L;
+    else if (rc == VTK_ERR_NOMEM) A->ctx->err.clear();   // no memory for the tables: not detected
     else if (rc != VTK_ERR_ARG) return rc;
     return VTK_OK;
 }
@@ -1041,9 +1057,12 @@ bool cyc_ring_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M, bool bj) {
 }
 
 // the 4D grid rows' cycle-start residual through k_g4_ring (tunings g4_ring, g4_res; BJ(8) tridiag)
+// (only for grids whose window and tables fit the kernel's LDS, g4_ring_fits; larger 4D
+// grids keep the SELL grid-row kernels)
 bool g4_resid_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M) {
     return A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && c->tune.g4_res && A->use_sell &&
-           A->sell.uniform_w > 8 && M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr;
+           A->sell.uniform_w > 8 && M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr &&
+           g4_ring_fits(A->g4, A->n_local, c->tune.g4_gr, 3);
 }
 
 int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0,
@@ -1099,12 +1118,17 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // there the SpMV + BJ kernel and the streaming dots kernel beat the register-capped fused
     // kernel (C4: 707 + 658 us vs 1473 us per step, 422 vs 405 it/s)
     // (with the 4D grid rows (Grid4) the fused kernel loads no values or codes: tuning c4_fused)
-    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused && c->tune.g4_ring <= 0;   // C4 A/B: 213.8 -> 210.3 ms
+    const bool g4_fits = s.A->d_g4tab && g4_ring_fits(s.A->g4, n, c->tune.g4_gr, 0);
+    const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused && (c->tune.g4_ring <= 0 || !g4_fits);   // C4 A/B: 213.8 -> 210.3 ms
     // grid rows with x staged through LDS (k_g4_ring) for the split step's SpMV + BJ
+    // (every mode the cycle launches fits when mode 0 fits: g4_ring_group)
     const bool g4_ring = s.A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && s.A->use_sell && s.M &&
-                         s.M->kind == VTK_PREC_BJACOBI && s.M->bs == 8 && bj_op(s.M).tri != nullptr;
+                         s.M->kind == VTK_PREC_BJACOBI && s.M->bs == 8 && bj_op(s.M).tri != nullptr && g4_fits;
     const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M) && !g4_fused;
-    const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9;
+    // the ring step also across ranks: interior groups while the halo planes
+    // are in flight, the boundary planes' groups once they have landed
+    const bool ring4 = g4_ring && s.A->use_sell && s.A->sell.uniform_w > 8 && !g4_fused;
+    const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9 && !ring4;
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
     const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
                          s.M->line.seg <= 32 && s.G <= GMAX;
@@ -1227,8 +1251,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
               HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, s.p_of(j), s.dcpart, s.G, stop, j, c->stream)); }
             cnt = s.G;
-        } else if (g4_ring && wide9) {
-            TRY(halo_exchange(s.A, pj));
+        } else if (ring4) {
             // g4_dc: the step's dots in the same sweep (+ V_j; w is still written for the update)
             G4Dots dd;
             dd.V = s.V;
@@ -1238,13 +1261,53 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             // g4_dc: every step's dots fused in; step 0's (|p|^2, p.w, |w|^2 only) by default
             const bool dc = c->tune.g4_dc != 0 || (j == 0 && c->tune.g4_dc0 != 0);
             dd.mode = c->tune.g4_dc != 0 ? 1 : 2;
-            Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j,
-                    solver_matrix_bytes(s.A) + b_inv + 2 * n8 + (dc ? n8 * j : 0.0));   // D, m, x, w (+ V_j)
-            int grid = 0;
-            HIPCHK(c, launch_g4_ring(s.A->g4, pj, s.A->g4.lblk >= 0 ? s.A->d_halo : nullptr, s.M->d_tri + s.M->tri_ld, s.w, n,
-                                     s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, dc ? &dd : nullptr,
-                                     &grid, stop, j, c->stream));
-            if (dc) cnt = grid;
+            const double b_ring = solver_matrix_bytes(s.A) + b_inv + 2 * n8 + (dc ? n8 * j : 0.0);   // D, m, x, w (+ V_j)
+            const double *halo = s.A->g4.lblk >= 0 ? s.A->d_halo : nullptr;
+            const double *mt = s.M->d_tri + s.M->tri_ld;
+            if (!halo || !bj_split(s.M)) {
+                TRY(halo_exchange(s.A, pj));
+                Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring);
+                int grid = 0;
+                HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd,
+                                         c->tune.g4_xcd, c->tune.g4_gr, dc ? &dd : nullptr, &grid, stop, j, c->stream));
+                if (dc) cnt = grid;
+            } else {
+                // across ranks: the rows [S4, n - S4) read no halo plane -- their groups run while
+                // the exchange is in flight (comm stream), the first / last plane's groups after it
+                // lands; the partials of the three launches side by side
+                const int mode = dc ? dd.mode : 0;
+                const int G = g4_ring_group(c->tune.g4_gr, mode);
+                const int64_t S4 = (int64_t)s.A->g4.Ny * s.A->g4.Nvx * s.A->g4.Nvy, ng = (n + G - 1) / G;
+                int64_t gi_lo = (S4 + G - 1) / G, gi_hi = (n - S4) / G;
+                if (gi_hi <= gi_lo) gi_lo = gi_hi = 0;   // no interior group: all after the exchange
+                const int64_t wgs = std::max(1, c->tune.g4_ring);
+                const int per = (int)std::max<int64_t>({1, (ng + wgs - 1) / wgs, mode ? (ng + GMAX - 4) / (GMAX - 3) : 1});
+                const bool exch = s.A->n_send > 0 || s.A->n_halo > 0 || c->host_comm;
+                if (exch) TRY(halo_exchange_async(s.A, pj));
+                int gin = 0, gb0 = 0, gb1 = 0;
+                {
+                    Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring * (double)(gi_hi - gi_lo) * G / std::max<double>(1.0, (double)n));
+                    if (gi_hi > gi_lo)
+                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, 0,
+                                                 c->tune.g4_gr, dc ? &dd : nullptr, &gin, stop, j, c->stream, (int)gi_lo,
+                                                 (int)gi_hi, per));
+                }
+                if (exch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+                {
+                    Prof pf(c, "spmv_bj_bd", j, b_ring * std::max(0.0, 1.0 - (double)(gi_hi - gi_lo) * G / std::max<double>(1.0, (double)n)));
+                    dd.part_off = gin;
+                    HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, 0,
+                                             c->tune.g4_gr, dc ? &dd : nullptr, &gb0, stop, j, c->stream, 0,
+                                             (int)(gi_hi > gi_lo ? gi_lo : ng), per));
+                    if (gi_hi > gi_lo) {
+                        dd.part_off = gin + gb0;
+                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, 0,
+                                                 c->tune.g4_gr, dc ? &dd : nullptr, &gb1, stop, j, c->stream, (int)gi_hi,
+                                                 (int)ng, per));
+                    }
+                }
+                if (dc) cnt = gin + gb0 + gb1;
+            }
         } else {
             Red h0, d0;
             TRY(precond_matvec(s, pj, s.w, stop, j, h0, d0, false));
@@ -1527,6 +1590,13 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             HIPCHK(c, launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
                                      c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, &dd, &g, nullptr,
                                      0, c->stream));
+            // across ranks the all-reduced partial vectors must have one length on every rank
+            // (the ring's grid follows the slab): zero-pad to GMAX, as every other reducing launch
+            if (c->dist && g < GMAX) {
+                HIPCHK(c, hipMemsetAsync(prr + g, 0, (size_t)(GMAX - g) * sizeof(double), c->stream));
+                HIPCHK(c, hipMemsetAsync(prz + g, 0, (size_t)(GMAX - g) * sizeof(double), c->stream));
+                g = GMAX;
+            }
             rr = reduce(c, prr, g, rc2);
             TRY(rc2);
             rz = reduce(c, prz, g, rc2);

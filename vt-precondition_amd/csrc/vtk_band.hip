@@ -35,17 +35,9 @@ namespace vtk {
 // ------------------------------------------------------------------------------------------
 // canonical line-band rows: canon_order (vtk_device.hpp)
 
-constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
-// geometry GEO: 2 = half lines (LP <= 400 rows, 7 waves, ~79 KB LDS, 2 workgroups per CU);
-// 4 = quarter lines (LP <= 200, 4 waves, ~40 KB, 4 per CU); the host plans with the GEO 2
-// constants (vtk_internal.hpp BAND_LP / BAND_T / BAND_WPC, vtk_line_band_plan)
-template <int GEO> struct BandGeo;
-template <> struct BandGeo<2> { static constexpr int LP = BAND_LP, T = BAND_T, WPC = BAND_WPC; };
-template <> struct BandGeo<4> { static constexpr int LP = 200, T = 256, WPC = 4; };
-#ifndef VTK_BAND_GEO
-#define VTK_BAND_GEO 2
-#endif
-static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 2 constants");
+// geometry: half lines (LP <= BAND_LP = 400 rows, 7 waves, ~79 KB LDS, two workgroups per CU).
+// Quarter lines with the staged basis double-buffered and every step's next line prefetched
+// (4 waves, 2-4 workgroups per CU by LDS) measured 2-10 % slower per step (round 5).
 #ifndef VTK_BAND_DOTS_UNROLL
 #define VTK_BAND_DOTS_UNROLL 2   // the dots' 64-row passes issued together (LDS latency once per group)
 #endif
@@ -57,8 +49,9 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
                                 // this many (0: the out-of-line call; C3 xupdate 648-653 -> 641-643 us)
 #endif
 #ifndef VTK_BAND_PF
-#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 10)   // j <= this: next line's update operands prefetched across SpMV + dots
-                                                 // (10: 567-570 us; 8: 570; 12: 567; 18: 624, spills)
+#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 12)   // j <= this: next line's update operands prefetched across SpMV + dots
+                                                 // (round 3: 10: 567-570 us; 8: 570; 12: 567; 18: 624, spills;
+                                                 // with the fused multiply-adds j <= 12 fits 124 VGPRs)
 #endif
 #ifndef VTK_BAND_GHT
 #define VTK_BAND_GHT 1   // one rank (no ghost lines): the instantiation without the ghost paths
@@ -82,10 +75,16 @@ static_assert(VTK_BAND_GEO == 2, "the host plans the band geometry with the GEO 
 // OPT bit 1 (WPC3): registers capped for 3 workgroups per CU (6 waves per SIMD) -- the low-J
 // launches, whose LDS (ring + (J + 1) staged basis rows) leaves room for a third workgroup and
 // whose serial line walks are latency-bound; the host plans 1.5x the line ranges for them.
+// The update's sums and the dots are fused multiply-adds (one rounding per term, half the f64
+// VALU instructions of the separate multiply and add; C3 solve -1 %, round 5); p_j's recompute
+// (here and in the x update's) is the same fused chain, so step j forms p_j exactly as step j-1
+// did.  (k_dc_update keeps the unfused operations of the oracle's sequence.)
 template <int OPT> constexpr int band_wpe() { return (OPT & 2) ? 6 : 4; }
-template <int WU, int J, int GEO, int VMODE = 0, bool GH = true, int OPT = 0>
-__global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu(band_wpe<OPT>()))) void k_band_step(BandK a) {
-    constexpr int BAND_LP = BandGeo<GEO>::LP, BAND_T = BandGeo<GEO>::T, BAND_RS = BAND_T;
+__device__ __forceinline__ double band_msub(double acc, double a, double b) { return __builtin_fma(-a, b, acc); }
+__device__ __forceinline__ double band_madd(double acc, double a, double b) { return __builtin_fma(a, b, acc); }
+template <int WU, int J, int VMODE = 0, bool GH = true, int OPT = 0>
+__global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe<OPT>()))) void k_band_step(BandK a) {
+    constexpr int BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
     __shared__ double vbuf[VTK_BAND_REREAD ? 1 : (VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
     __shared__ double ring[4 * BAND_RS];
@@ -95,8 +94,8 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
     constexpr int j = J;
     if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
         if constexpr (VTK_BAND_XUP_INLINE > 0)
-            dc_xupdate_body<VTK_BAND_XUP_INLINE>(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf,
-                                                 a.x, a.H, a.S, a.m, a.w_prev);
+            dc_xupdate_body<VTK_BAND_XUP_INLINE, true>(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf,
+                                                     a.x, a.H, a.S, a.m, a.w_prev);
         else
             dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, a.w_prev);
         return;
@@ -213,19 +212,19 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         if (j >= 1) {
             double tp = o.wm;
 #pragma unroll
-            for (int k = 0; k < J; ++k) tp = tp - cp[k] * vreg[k];
+            for (int k = 0; k < J; ++k) tp = band_msub(tp, cp[k], vreg[k]);
             pj = tp * qp;
         }
         double av = pj, tv = o.wj;
 #pragma unroll
         for (int k = 0; k < J; ++k) {
             const double sk = cs[k], ek = ce[k];
-            av = av - sk * vreg[k];
-            tv = tv - ek * vreg[k];
+            av = band_msub(av, sk, vreg[k]);
+            tv = band_msub(tv, ek, vreg[k]);
         }
         double vj = pj;
         if (j >= 1) vj = av * rinv;
-        tv = tv - ej * vj;
+        tv = band_msub(tv, ej, vj);
         const double pn = tv * qc;
         vreg[J] = vj;
         if (kind == 0 && own) {
@@ -237,10 +236,10 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
         }
         return pn;
     };
-    auto stage = [&]() {
+    auto stage = [&](double *vb) {
         if (!VTK_BAND_REREAD && own) {
 #pragma unroll
-            for (int k = 0; k <= J; ++k) vbuf[k * BAND_LP + tid - 8] = vreg[k];
+            for (int k = 0; k <= J; ++k) vb[k * BAND_LP + tid - 8] = vreg[k];
         }
     };
     auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
@@ -412,22 +411,22 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
 #pragma unroll VTK_BAND_DOTS_UNROLL
                     for (int t = lane; t < LP; t += 64) {
                         const double vv = vk[t];
-                        acc[u][0] += vv * pr[t];
-                        acc[u][1] += vv * wbuf[t];
+                        acc[u][0] = band_madd(acc[u][0], vv, pr[t]);
+                        acc[u][1] = band_madd(acc[u][1], vv, wbuf[t]);
                     }
                 } else if (itm == j + 1) {
 #pragma unroll VTK_BAND_DOTS_UNROLL
                     for (int t = lane; t < LP; t += 64) {
                         const double pv = pr[t], wq = wbuf[t];
-                        acc[u][0] += pv * pv;
-                        acc[u][1] += pv * wq;
-                        acc[u][2] += wq * wq;
+                        acc[u][0] = band_madd(acc[u][0], pv, pv);
+                        acc[u][1] = band_madd(acc[u][1], pv, wq);
+                        acc[u][2] = band_madd(acc[u][2], wq, wq);
                     }
                 }
             }
             __syncthreads();
         }
-        if (it >= 1 && it <= nl) stage();   // line y is owned: its basis rows for the dots one line on
+        if (it >= 1 && it <= nl) stage(vbuf);   // line y is owned: its basis rows for the dots one line on
     }
     // per-workgroup partials in launch_dc_dots' layout for step j+1
 #pragma unroll
@@ -458,19 +457,18 @@ __global__ __launch_bounds__(BandGeo<GEO>::T) __attribute__((amdgpu_waves_per_eu
 // the one-rank production instantiations (canonical rows, line-separable values) with the
 // variant bits of a.opt; WPC3 only where the LDS of three workgroups fits (J <= BAND_J3)
 template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipStream_t s) {
-    const dim3 g(grid), blk(BandGeo<VTK_BAND_GEO>::T);
+    const dim3 g(grid), blk(BAND_T);
     if constexpr (J <= BAND_J3) {
         if (J > a.j3) {}
-        else if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false, 3>), g, blk, 0, s, a); return; }
-        if ((a.opt & 3) == 2) { hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false, 2>), g, blk, 0, s, a); return; }
+        else if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 3>), g, blk, 0, s, a); return; }
+        if ((a.opt & 3) == 2) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 2>), g, blk, 0, s, a); return; }
     }
-    if (a.opt & 1) hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false, 1>), g, blk, 0, s, a);
-    else hipLaunchKernelGGL((k_band_step<5, J, VTK_BAND_GEO, 2, false>), g, blk, 0, s, a);
+    if (a.opt & 1) hipLaunchKernelGGL((k_band_step<5, J, 2, false, 1>), g, blk, 0, s, a);
+    else hipLaunchKernelGGL((k_band_step<5, J, 2, false>), g, blk, 0, s, a);
 }
 
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
-    constexpr int lp = BandGeo<VTK_BAND_GEO>::LP;
-    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > lp || (a.L / a.H_parts) % 8 != 0 ||
+    if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > BAND_LP || (a.L / a.H_parts) % 8 != 0 ||
         a.j + 1 > BAND_JV || grid < a.H_parts || grid > GMAX || grid % a.H_parts != 0 || grid / a.H_parts > a.X ||
         a.n > INT32_MAX / 2)
         return hipErrorInvalidValue;
@@ -478,9 +476,9 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
         if (a.lsv && a.canon && VTK_BAND_GHT && !a.ghost) launch_band_one_rank<J_>(a, grid, s); \
-        else if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 2>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
-        else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO, 1>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
-        else hipLaunchKernelGGL((k_band_step<5, J_, VTK_BAND_GEO>), dim3(grid), dim3(BandGeo<VTK_BAND_GEO>::T), 0, s, a); \
+        else if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, 2>), dim3(grid), dim3(BAND_T), 0, s, a); \
+        else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, 1>), dim3(grid), dim3(BAND_T), 0, s, a); \
+        else hipLaunchKernelGGL((k_band_step<5, J_>), dim3(grid), dim3(BAND_T), 0, s, a); \
         break;
         VTK_BAND_J(0) VTK_BAND_J(1) VTK_BAND_J(2) VTK_BAND_J(3) VTK_BAND_J(4) VTK_BAND_J(5) VTK_BAND_J(6)
         VTK_BAND_J(7) VTK_BAND_J(8) VTK_BAND_J(9) VTK_BAND_J(10) VTK_BAND_J(11) VTK_BAND_J(12) VTK_BAND_J(13)
@@ -867,11 +865,11 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
 // p.w, |w|^2, each lane over its own rows); 3 the cycle-start residual r = b - A x, w = M^-1 r,
 // |r|^2, |w|^2 (partials p0, p1) -- k_sell<EPI_RESID_PREC>'s operations.  Modes 1-3: one partial
 // per workgroup, lanes -> waves -> workgroup in a fixed order.
-constexpr int G4TAB = 1024;
 template <typename VT, bool HALO, int RL, int PD, int MODE, int GR>
 __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 && RL <= 5120 && MODE != 1 ? 6 : 1))) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
                                                 const double *__restrict__ mtri, double *__restrict__ w, int n,
-                                                int ngroups_per_wg, G4Dots dd, const int *stop_col, int col) {
+                                                int ngroups_per_wg, int g_lo, int g_hi, G4Dots dd, const int *stop_col,
+                                                int col) {
     constexpr bool DC = MODE == 1, RES = MODE == 3;
     __shared__ double ring[RL];
     __shared__ double tb[G4TAB];
@@ -886,9 +884,17 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
     const int tid = threadIdx.x, lane = tid & 63, ii = lane & 7;
     const int Nvy = g.Nvy, Nvx = g.Nvx, Ny = g.Ny;
     const int S2 = Nvy, S3 = Nvx * Nvy, S4 = Ny * S3;
-    const int ng = (n + (GR - 1)) / GR;
-    const int gb = blockIdx.x * ngroups_per_wg, ge = min(ng, gb + ngroups_per_wg);
-    if (gb >= ge) return;
+    const int gb = g_lo + blockIdx.x * ngroups_per_wg, ge = min(g_hi, gb + ngroups_per_wg);
+    const int pslot = dd.part_off + blockIdx.x;   // this workgroup's partial slot
+    if (gb >= ge) {   // (no work: zero partials, so that the slots' consumers need no count)
+        if (MODE >= 1 && threadIdx.x < DC_NQ) {
+            const int q = threadIdx.x;
+            if (MODE == 3) { if (q == 0) dd.p0[pslot] = 0.0; if (q == 1) dd.p1[pslot] = 0.0; }
+            else if (MODE == 2 ? q >= 2 * DC_MAXJ : (q < dd.j || (q >= DC_MAXJ && q < DC_MAXJ + dd.j) || q >= 2 * DC_MAXJ))
+                dd.part[(size_t)q * GMAX + pslot] = 0.0;
+        }
+        return;
+    }
     const int oy = 2 * Nvx, ovx = oy + 2 * Nvy, ovy = ovx + 2 * g.X;
     const int lb = g.lblk;
     // the value tables in LDS (a table load in the row loop would be a global load issued after
@@ -1081,7 +1087,7 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
         __syncthreads();
         for (int q = tid; q < DC_NQ; q += GR) {
             const bool used = q < dd.j || (q >= DC_MAXJ && q < DC_MAXJ + dd.j) || q >= 2 * DC_MAXJ;
-            if (used) dd.part[(size_t)q * GMAX + blockIdx.x] = red[q];
+            if (used) dd.part[(size_t)q * GMAX + pslot] = red[q];
         }
     }
     if constexpr (MODE >= 2) {
@@ -1097,22 +1103,21 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
             double sum = 0.0;
 #pragma unroll
             for (int wv = 0; wv < GR / 64; ++wv) sum += red3[tid][wv];
-            if constexpr (MODE == 2) dd.part[(size_t)(2 * DC_MAXJ + tid) * GMAX + blockIdx.x] = sum;
-            else if (tid == 0) dd.p0[blockIdx.x] = sum;
-            else if (tid == 1) dd.p1[blockIdx.x] = sum;
+            if constexpr (MODE == 2) dd.part[(size_t)(2 * DC_MAXJ + tid) * GMAX + pslot] = sum;
+            else if (tid == 0) dd.p0[pslot] = sum;
+            else if (tid == 1) dd.p1[pslot] = sum;
         }
     }
 }
 
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
                           int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out,
-                          const int *stop_col, int col, hipStream_t s) {
+                          const int *stop_col, int col, hipStream_t s, int g_lo, int g_hi, int per_in) {
     // gr: rows per group = lanes per workgroup (256, or 512 without the fused dots of mode 1)
     const int mode = dots ? dots->mode : 0;
-    const int G = gr >= 512 && mode != 1 ? 512 : 256;
+    const int G = g4_ring_group(gr, mode);
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy, S4 = S3 * g.Ny;
-    if (!g.tab || !g.D || 2 * S3 + 2 * G > 8192 || n <= 0 || n > INT32_MAX / 2 || S4 <= 0 || n % S4 ||
-        2 * (g.Nvx + g.Nvy + g.X + g.Ny) > G4TAB || (halo == nullptr) != (g.lblk < 0))
+    if (!g.tab || !g.D || !g4_ring_fits(g, n, gr, mode) || S4 <= 0 || n % S4 || (halo == nullptr) != (g.lblk < 0))
         return hipErrorInvalidValue;
     // the ring: the window 2 S3 + G plus the next group's rows
     const bool small = 2 * S3 + 2 * G <= (G == 256 ? 4608 : 5120);
@@ -1124,7 +1129,14 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
     if (xcd > 0) per = std::max<int64_t>(1, (S4 + G / 2 * xcd) / (G * (int64_t)xcd));
     // the fused reductions write one partial per workgroup: at most GMAX workgroups
     if (mode) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
-    const dim3 grid((unsigned)((ng + per - 1) / per)), blk(G);
+    // a group range [g_lo, g_hi) of the launch (the interior / boundary planes of a rank's slab
+    // around the halo exchange), groups per workgroup per_in > 0 as the caller planned them
+    if (g_hi < 0) g_hi = (int)ng;
+    if (per_in > 0) per = per_in;
+    if (g_lo < 0 || g_lo > g_hi || g_hi > ng) return hipErrorInvalidValue;
+    const int64_t span = std::max<int64_t>(1, g_hi - g_lo);
+    const dim3 grid((unsigned)((span + per - 1) / per)), blk(G);
+    if (mode && (dots->part_off < 0 || dots->part_off + (int64_t)grid.x > GMAX)) return hipErrorInvalidValue;
     if (mode < 0 || mode > 3 || (mode == 1 && (dots->j < 0 || dots->j > DC_MAXJ || !dots->V || !dots->part)) ||
         (mode == 2 && !dots->part) || (mode == 3 && (!dots->b || !dots->p0 || !dots->p1)))
         return hipErrorInvalidValue;
@@ -1132,7 +1144,7 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
     const G4Dots dd = dots ? *dots : G4Dots{};
 #define VTK_G4R(VT_, H_, RL_, PD_, DC_, GR_) \
     hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, PD_, DC_, GR_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, \
-                       dd, stop_col, col)
+                       g_lo, g_hi, dd, stop_col, col)
 #define VTK_G4R_M(VT_, H_, RL_, GR_) \
     do { \
         if (mode == 1) VTK_G4R(VT_, H_, RL_, 1, 1, GR_); \

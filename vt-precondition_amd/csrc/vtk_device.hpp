@@ -397,7 +397,8 @@ __device__ inline void hess_solve(const double *__restrict__ H, const double *__
 // c = stop_col is j-1 (column j-1 finalised in step j: V[0..j-1] all stored) or j (column j
 // committed early: v_j = (p_j - V_j s) / r formed here exactly as the normal pass would store
 // it).  Same operations and order as k_xupdate, so x is bit-identical to the unfused path.
-template <int XB>
+// FM: p_j's recompute and v_j's formation as fused multiply-adds (k_band_step's form)
+template <int XB, bool FM = false>
 static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict__ V, int64_t ld, int j, int c,
                                                        int64_t n, const DcCoef *cf, double *__restrict__ x,
                                                        const double *__restrict__ H, const double *__restrict__ S,
@@ -440,14 +441,14 @@ static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict_
                     for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
 #pragma unroll
                     for (int u = 0; u < XB; ++u) {
-                        tx = tx - ep[k + u] * v[u].x;
-                        ty = ty - ep[k + u] * v[u].y;
+                        tx = FM ? __builtin_fma(-ep[k + u], v[u].x, tx) : tx - ep[k + u] * v[u].x;
+                        ty = FM ? __builtin_fma(-ep[k + u], v[u].y, ty) : ty - ep[k + u] * v[u].y;
                     }
                 }
                 for (; k < j; ++k) {
                     const d2v v = ldnt2(V + (size_t)k * ld + i);
-                    tx = tx - ep[k] * v.x;
-                    ty = ty - ep[k] * v.y;
+                    tx = FM ? __builtin_fma(-ep[k], v.x, tx) : tx - ep[k] * v.x;
+                    ty = FM ? __builtin_fma(-ep[k], v.y, ty) : ty - ep[k] * v.y;
                 }
                 a = make_double2(tx * qp, ty * qp);
             } else if (c == j) {
@@ -459,8 +460,8 @@ static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict_
                 ay += ys[k] * v.y;
                 if (c == j) {
                     const double sk = cs[k];
-                    a.x = a.x - sk * v.x;
-                    a.y = a.y - sk * v.y;
+                    a.x = FM ? __builtin_fma(-sk, v.x, a.x) : a.x - sk * v.x;
+                    a.y = FM ? __builtin_fma(-sk, v.y, a.y) : a.y - sk * v.y;
                 }
             };
             int k = 0;
@@ -486,13 +487,13 @@ static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict_
             double ax = 0.0, a = c == j ? pj[i] : 0.0;
             if (rec) {
                 double t = wprev[i];
-                for (int k = 0; k < j; ++k) t = t - ep[k] * V[(size_t)k * ld + i];
+                for (int k = 0; k < j; ++k) t = FM ? __builtin_fma(-ep[k], V[(size_t)k * ld + i], t) : t - ep[k] * V[(size_t)k * ld + i];
                 a = t * qp;
             }
             for (int k = 0; k < kv; ++k) {
                 const double v = V[(size_t)k * ld + i];
                 ax += ys[k] * v;
-                if (c == j) a = a - cs[k] * v;
+                if (c == j) a = FM ? __builtin_fma(-cs[k], v, a) : a - cs[k] * v;
             }
             if (c == j) ax += ys[j] * (j >= 1 ? a * rinv : a);
             x[i] = x[i] + ax;

@@ -73,11 +73,11 @@ bool vlasov_params_ok(const vtk_vlasov_params *p) { return valid_params(p); }
 using namespace vtk;
 
 namespace vtk {
-// parts of a line of L rows for the band step: the fewest equal parts of <= BAND_LP rows, each
+// parts of a line of L rows for the band step: the fewest equal parts of <= lp rows, each
 // a multiple of 8 rows (whole BJ blocks); 0 when there is none
-int band_parts(int64_t L) {
-    for (int h = 1; h <= 16; ++h)
-        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= BAND_LP) return h;
+int band_parts(int64_t L, int lp) {
+    for (int h = 1; h <= 32; ++h)
+        if (L % h == 0 && (L / h) % 8 == 0 && L / h <= lp) return h;
     return 0;
 }
 

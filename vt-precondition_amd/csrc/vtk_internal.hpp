@@ -135,6 +135,16 @@ struct Grid4 {
     const void *D = nullptr;       // diagonal per row, the operator's value type
 };
 inline size_t grid4_tab_len(const Grid4 &g) { return 2 * ((size_t)g.Nvx + g.Nvy + g.X + g.Ny); }
+// k_g4_ring's limits (vtk_band.hip): the LDS table TX | TY | TVX | TVY of <= G4TAB doubles and a
+// ring of <= 8192 doubles holding the y-line window 2 S3 plus two groups of rows (512 per group for
+// gr >= 512 outside the fused-dots mode 1, else 256).  The solver takes the ring step only for grids
+// that fit (else the SELL grid-row kernels); launch_g4_ring refuses the others
+constexpr int G4TAB = 1024;
+inline int g4_ring_group(int gr, int mode) { return gr >= 512 && mode != 1 ? 512 : 256; }
+inline bool g4_ring_fits(const Grid4 &g, int64_t n, int gr, int mode) {
+    const int64_t S3 = (int64_t)g.Nvx * g.Nvy;
+    return n > 0 && n <= INT32_MAX / 2 && 2 * S3 + 2 * g4_ring_group(gr, mode) <= 8192 && grid4_tab_len(g) <= (size_t)G4TAB;
+}
 
 // Tuning switches of a context (vtk_ctx_set_tuning): the defaults are the
 // production path, the others exist for in-process A/B measurements and the bit-identity tests
@@ -471,9 +481,10 @@ struct BandK {
     int j3 = 0;                  // opt bit 1 applies to steps j <= j3 (<= BAND_J3)
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
-// geometry (k_band_step<..., GEO 2>): a workgroup of BAND_T threads owns <= BAND_LP rows of a
+// geometry (k_band_step): a workgroup of BAND_T threads owns <= BAND_LP rows of a
 // line (one part; parts per line = band_parts), BAND_WPC workgroups per CU (LDS-bound)
 constexpr int BAND_LP = 400, BAND_T = 448, BAND_WPC = 2;
+constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
 // band steps j <= BAND_J3 may run three workgroups per CU (Tuning::band_opt bit 1): their LDS
 // (ring + (j + 1) staged basis rows of BAND_LP doubles) fits three times into 160 KB
 constexpr int BAND_J3 = 4;   // (instantiated up to here; beyond j = 2 the 80-VGPR cap spills)
@@ -485,7 +496,7 @@ hipError_t launch_ghost_pack(const double *V, int64_t ld, int j, const double *w
                              int64_t off_first, int64_t off_last, hipStream_t s);
 hipError_t launch_ghost_unpack(const double *rbuf, int64_t off_left, int64_t off_right, int j, int m, int L,
                                double *ghost, hipStream_t s);
-int band_parts(int64_t L);    // parts per line (rows per part <= BAND_LP, multiple of 8); 0: none (vtk_host.cpp)
+int band_parts(int64_t L, int lp = BAND_LP);   // parts per line (rows per part <= lp, multiple of 8); 0: none (vtk_host.cpp)
 // *bad |= 1 when some column is outside the lines x-1..x+1 (mod X) of its row, |= 2 when one is
 // more than one row off its row's position in the line (bad zeroed by the caller)
 // line-separable values (vtk_csr::d_lsv): build D | TX | TV from the CSR, then *bad |= 1 when
@@ -547,10 +558,12 @@ struct G4Dots {
     double *part = nullptr;        // modes 1, 2: the dots partials (launch_dc_dots' layout)
     const double *b = nullptr;     // mode 3: the right-hand side; |r|^2, |w|^2 partials
     double *p0 = nullptr, *p1 = nullptr;
+    int part_off = 0;              // the launch's first partial slot (split launches side by side)
 };
+// g_lo, g_hi: the group range (GR-row groups; -1: all), per: groups per workgroup (0: from wgs)
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
                           int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
-                          int col, hipStream_t s);
+                          int col, hipStream_t s, int g_lo = 0, int g_hi = -1, int per = 0);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 

@@ -45,6 +45,11 @@ class HostComm:
         self.group = group
         self.world = dist.get_world_size(group)
         self.errors = []
+        # every communicator operation the library issued, in order: ("allreduce", count),
+        # ("alltoallv", elem_bytes, send counts per peer, recv counts per peer), ("allgather",
+        # bytes) -- the sequence the RCCL transport would issue at the same points (DESIGN.md §6:
+        # every rank must issue the same collectives, and matched send/recv pairs)
+        self.log = []
         self._cbs = (ALLRED(self._allreduce), A2AV(self._alltoallv), AGATH(self._allgather))
         self.struct = _HostCommStruct(None, *self._cbs)
 
@@ -57,6 +62,8 @@ class HostComm:
             return 1
 
     def _allreduce(self, user, buf, count):
+        self.log.append(("allreduce", int(count)))
+
         def go():
             import torch
             a = np.ctypeslib.as_array(buf, shape=(count,))
@@ -65,6 +72,9 @@ class HostComm:
         return self._guard(go)
 
     def _alltoallv(self, user, sb, scnt, soff, rb, rcnt, roff, eb):
+        self.log.append(("alltoallv", int(eb), [int(scnt[q]) for q in range(self.world)],
+                         [int(rcnt[q]) for q in range(self.world)]))
+
         def go():
             import torch
             W = self.world
@@ -79,6 +89,8 @@ class HostComm:
         return self._guard(go)
 
     def _allgather(self, user, sb, rb, nbytes):
+        self.log.append(("allgather", int(nbytes)))
+
         def go():
             import torch
             W = self.world
@@ -89,6 +101,28 @@ class HostComm:
             for q in range(W):
                 rv[q * nbytes:(q + 1) * nbytes] = outs[q].numpy()
         return self._guard(go)
+
+
+def check_sequences(logs) -> int:
+    """Every rank's communicator log (HostComm.log, rank order) describes one run that RCCL could
+    execute: the same operation kinds and sizes at every position on every rank, and at every
+    alltoallv each send count matched by the peer's receive count (a rank with no neighbours
+    takes part with zero counts).  Returns the number of operations; AssertionError otherwise."""
+    W = len(logs)
+    n = len(logs[0])
+    assert all(len(lg) == n for lg in logs), [len(lg) for lg in logs]
+    for i in range(n):
+        ops = [lg[i] for lg in logs]
+        kind = ops[0][0]
+        assert all(o[0] == kind for o in ops), (i, [o[0] for o in ops])
+        if kind == "alltoallv":
+            assert all(o[1] == ops[0][1] for o in ops), (i, "element size")
+            for r in range(W):
+                for q in range(W):
+                    assert ops[r][2][q] == ops[q][3][r], (i, r, q, ops[r][2][q], ops[q][3][r])
+        else:
+            assert all(o[1] == ops[0][1] for o in ops), (i, kind, [o[1] for o in ops])
+    return n
 
 
 def init_host(ctx, rank: int, world: int, group=None) -> HostComm:

@@ -73,6 +73,8 @@ class SolverConfig:
     device: int
     report: str
     line_len: int | None = None   # operator/line_len: None (absent / "auto") = detected by vtk_csr_create
+    gpus: int = 1                 # run/gpus: ranks, one process per GPU (absent: 1)
+    comm: str = "rccl"            # run/comm: rccl, or host (host-staged, ranks may share a GPU)
 
     @classmethod
     def load(cls, path: str = DEFAULT_XML, **overrides) -> "SolverConfig":
@@ -99,6 +101,8 @@ class SolverConfig:
                   report=t.get_node_value("run/report"))
         ll = t.get_optional("operator/line_len", "auto").lower()
         cfg.line_len = None if ll in ("", "auto") else int(ll)
+        cfg.gpus = int(t.get_optional("run/gpus", "1") or 1)
+        cfg.comm = (t.get_optional("run/comm", "rccl") or "rccl").lower()
         for k, v in overrides.items():
             if v is not None:
                 setattr(cfg, k, v)
@@ -106,4 +110,20 @@ class SolverConfig:
             raise ValueError(f"unknown preconditioner {cfg.preconditioner!r}")
         if cfg.orth not in ("auto", "mgs", "dcgs2"):
             raise ValueError(f"unknown orthogonalisation {cfg.orth!r}")
+        if cfg.gpus < 1:
+            raise ValueError(f"run/gpus must be >= 1, got {cfg.gpus}")
+        if cfg.comm not in ("rccl", "host"):
+            raise ValueError(f"unknown run/comm {cfg.comm!r} (rccl, host)")
         return cfg
+
+    def slab_align(self) -> int:
+        """Row-partition granule: whole x-slabs (a 2D x-line of Nv rows, a 4D x-plane of
+        Ny Nvx Nvy rows), so that the band step and the 4D grid rows run across ranks; 1 for an
+        operator file unless operator/line_len names its line length."""
+        if self.operator_file:
+            return self.line_len or 1
+        if self.dim == 2:
+            return self.shape[1]
+        if self.dim == 4:
+            return self.shape[1] * self.shape[2] * self.shape[3]
+        return 1
