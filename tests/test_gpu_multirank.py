@@ -74,7 +74,7 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
     gip, gix, gd = A.download()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), y=y, inv=inv, x=xs, info=info,
              iters=st.inner_iters, rb=rb, re=re_, halo=A.n_halo, gip=gip, gix=gix, gd=gd, band=st.band,
-             line_band=A.line_band,
+             line_band=A.line_band, line_values=A.line_values,
              errors=np.array(hc.errors, dtype=object).astype(str), classes=json.dumps(classes),
              commlog=json.dumps(hc.log))
     dist.barrier()
@@ -119,6 +119,9 @@ def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
         # 2D operators under DCGS2 run the line-band step across ranks (ghost lines exchanged)
         expect_band = p.dim == 2 and orth == "dcgs2"
         assert int(z["band"]) == int(expect_band), (int(z["band"]), int(z["line_band"]))
+        if p.dim == 2:   # separable values AND canonical rows on every rank (the halo lines' place
+            # in the global column order: canon_order_xv's xord), so every rank runs the code-free step
+            assert int(z["line_values"]) == 2, (r, int(z["line_values"]))
         assert int(z["info"]) == ref.info == 0
         assert abs(int(z["iters"]) - ref.inner_iters) <= 1
         xs[rb:re_] = z["x"]

@@ -54,7 +54,7 @@ def _worker(rank, world, port, case, outdir):
     np.save(os.path.join(outdir, f"x{rank}.npy"), x)
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), info=info, iters=st.inner_iters, band=st.band,
              rb=rb, re=re_, halo=A.n_halo, line_band=A.line_band, mode=M.mode, layout=A.layout_info()["layout"],
-             separable=A.line_separable,
+             separable=A.line_separable, line_values=A.line_values,
              errors=np.array(hc.errors, dtype=object).astype(str), commlog=json.dumps(hc.log))
     M.close()
     A.close()
@@ -82,6 +82,7 @@ def test_row_partitioned_full_size(tmp_path, golden_large, case, world):
             assert int(z["line_band"]) == p.shape[1] and int(z["halo"]) == 2 * p.shape[1]
             assert int(z["band"]) == 1
             assert bool(z["separable"])   # the distributed line-separable tables (halo lines)
+            assert int(z["line_values"]) == 2, (r, int(z["line_values"]))   # ... and canonical rows
         else:            # 4D: the halo is the two neighbour x-planes
             assert int(z["halo"]) == 2 * int(np.prod(p.shape[1:]))
         iters.append(int(z["iters"]))

@@ -369,6 +369,7 @@ SpmvIn lsv_in(SpmvIn in, const vtk_csr *A) {
         in.lsv = A->d_lsv;
         in.lsv_L = (int)A->band_L;
         in.lsv_lblk = A->band_ghost ? A->band_lblk : -1;
+        in.lsv_xord = A->band_ghost ? A->band_xord : 0;
         // tuning sell_canon 0 (A/B): the SELL codes even for canonical rows
         in.lsv_canon = A->lsv_canon && A->ctx->tune.sell_canon ? 1 : 0;
     }
@@ -691,6 +692,7 @@ void destroy_csr(vtk_csr *A) {
 // into `out`, which the caller commits only once the whole check has passed.
 struct BandLayout {
     int lblk = 0;
+    int xord = 0;   // bit 0: the slab starts at global line 0, bit 1: it ends at the last line
     int peer[2] = {-1, -1};
     std::vector<int64_t> scnt, soff, rcnt, roff;
     int64_t off_first = -1, off_last = -1, off_left = -1, off_right = -1;
@@ -712,6 +714,7 @@ int band_check_dist(vtk_csr *A, int64_t L, bool &solo, BandLayout &out) {
     }
     if (!((gl[0] == left && gl[1] == right) || (gl[0] == right && gl[1] == left))) return VTK_ERR_ARG;
     out.lblk = gl[0] == left ? 0 : 1;
+    out.xord = (A->row_begin == 0 ? 1 : 0) | (A->row_end == A->n_global ? 2 : 0);
     auto owner = [&](int64_t line) {
         for (int q = 0; q < c->world; ++q)
             if (A->offsets[q] <= line * L && line * L < A->offsets[q + 1]) return q;
@@ -803,7 +806,8 @@ int band_check_all(vtk_csr *A, int64_t L) {
         if (rc == VTK_OK && e == hipSuccess) e = hipMemsetAsync(bad.p, 0, sizeof(int), c->stream);
         if (rc == VTK_OK && e == hipSuccess)
             e = launch_lsv_build(A->d_indptr, A->d_indices, static_cast<const double *>(A->d_data), n, (int)L,
-                                 chk.ghost ? chk.lay.lblk : -1, lsv.as<double>(), bad.as<int>(), c->stream);
+                                 chk.ghost ? chk.lay.lblk : -1, chk.ghost ? chk.lay.xord : 0, lsv.as<double>(), bad.as<int>(),
+                                 c->stream);
         if (rc == VTK_OK && e == hipSuccess) e = hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream);
         if (rc == VTK_OK && e == hipSuccess) e = hipStreamSynchronize(c->stream);
         if (rc == VTK_OK && e != hipSuccess)
@@ -825,6 +829,7 @@ int band_check_all(vtk_csr *A, int64_t L) {
     A->band_vloc = chk.vloc;
     A->band_ghost = chk.ghost;
     A->band_lblk = chk.lay.lblk;
+    A->band_xord = chk.ghost ? chk.lay.xord : 0;
     A->band_peer[0] = chk.lay.peer[0];
     A->band_peer[1] = chk.lay.peer[1];
     A->band_scnt = chk.lay.scnt;
@@ -1242,7 +1247,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
                                           s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
-                                          c->stream, line_canon ? 1 : 0, c->tune.lsv_spmv_cap, c->tune.lsv_ring));
+                                          c->stream, line_canon ? 1 : 0, c->tune.lsv_spmv_cap, c->tune.lsv_ring,
+                                          s.A->band_ghost ? s.A->band_xord : 0));
             } else {
                 Prof pf(c, "spmv", j, b_csr + 2 * n8);
                 HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
@@ -1366,6 +1372,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.H_parts = s.band_H;
             a.ghost = s.ghost;
             a.left_blk = s.A->band_lblk;
+            a.xord = s.A->band_xord;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
             a.canon = band_lsv && s.A->lsv_canon && band_canon ? (canon_sl ? 2 : 1) : 0;
             a.opt = s.ghost ? 0 : c->tune.band_opt;   // variants exist for the one-rank instantiation

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                 // the line's stored order of the five kinds (the same for every lane of the line)
                 int64_t cxm, cxp;
                 const int ord = __builtin_amdgcn_readfirstlane(
-                    canon_order_xv(x, 0, a.n, L, X, GH && a.ghost ? a.left_blk : -1, cxm, cxp));
+                    canon_order_xv(x, 0, a.n, L, X, GH && a.ghost ? a.left_blk : -1, cxm, cxp, a.xord));
                 const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + 8;   // ring offset of line x
                 // the three orders the lines take (interior / first line / last line of one rank),
                 // straight-line: every lane reads its five operands (a clamped row off its own
@@ -601,7 +601,7 @@ __device__ __forceinline__ int lsv_slot(int64_t r, int64_t c, int64_t n, int L, 
 // the operator is separable; the check pass decides); pass 1: compare every entry bit for bit
 __global__ __launch_bounds__(NT) void k_lsv_build(const int32_t *__restrict__ indptr, const int32_t *__restrict__ indices,
                                                   const double *__restrict__ data, int64_t n, int L, int lblk,
-                                                  double *__restrict__ lsv, int *bad, int pass) {
+                                                  int xord, double *__restrict__ lsv, int *bad, int pass) {
     const int X = (int)(n / L);
     for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) {
         for (int k = indptr[r]; k < indptr[r + 1]; ++k) {
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(NT) void k_lsv_build(const int32_t *__restrict__ in
         if (pass == 1) {
             // |= 2: the row is not canonical (its stored columns differ from canon_order's)
             int64_t cxm, cxp;
-            const int ord = canon_order(r, n, L, X, lblk, cxm, cxp);
+            const int ord = canon_order(r, n, L, X, lblk, cxm, cxp, xord);
             const int64_t v = r % L;
             int k = indptr[r];
             bool ok = true;
@@ -633,13 +633,13 @@ __global__ __launch_bounds__(NT) void k_lsv_build(const int32_t *__restrict__ in
 }
 
 hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const double *data, int64_t n, int L,
-                            int lblk, double *lsv, int *bad, hipStream_t s) {
+                            int lblk, int xord, double *lsv, int *bad, hipStream_t s) {
     if (L <= 0 || n % L != 0 || n / L < 2) return hipErrorInvalidValue;
     int64_t g = (n + NT - 1) / NT;
     if (g > 4096) g = 4096;
     if (g < 1) g = 1;
     for (int pass = 0; pass < 2; ++pass) {
-        hipLaunchKernelGGL(k_lsv_build, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, data, n, L, lblk, lsv, bad, pass);
+        hipLaunchKernelGGL(k_lsv_build, dim3((unsigned)g), dim3(NT), 0, s, indptr, indices, data, n, L, lblk, xord, lsv, bad, pass);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -718,7 +718,7 @@ template <bool HALO, bool CANON = false>
 __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk, const int32_t *__restrict__ dict,
                                                  const double *__restrict__ lsv, const double *__restrict__ x,
                                                  const double *__restrict__ halo, double *__restrict__ y, int n, int L,
-                                                 int lblk, const int *stop_col, int col) {
+                                                 int lblk, int xord, const int *stop_col, int col) {
     if (stopped(stop_col, col)) return;
     const int lane = threadIdx.x & 63;
     const int X = n / L, nch = (n + 63) >> 6;
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(NT) void k_lsv_spmv(const uint32_t *__restrict__ pk
             if (act) {
                 int c[5];
                 double d[5];
-                canon_row(lsv, n, L, lblk, xl, v, drow, c, d);
+                canon_row(lsv, n, L, lblk, xl, v, drow, c, d, xord);
                 double xv[5];
 #pragma unroll
                 for (int k = 0; k < 5; ++k) {
@@ -1470,7 +1470,7 @@ hipError_t launch_lsv_ring_epi(int epi, const double *lsv, const double *x, cons
 
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
-                           hipStream_t s, int canon, int grid_cap, int ring_wgs) {
+                           hipStream_t s, int canon, int grid_cap, int ring_wgs, int xord) {
     if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || (halo && lblk < 0)) return hipErrorInvalidValue;
     if (ring_wgs > 0 && canon && !halo) {   // the LDS-staged form (one rank, canonical rows)
         const int H = band_parts(L);
@@ -1487,10 +1487,10 @@ hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double
     // 8.81 vs 8.70)
     const int64_t cap = grid_cap > 0 ? grid_cap : 8192;
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>((nch + 3) / 4, cap));
-    if (canon && halo) hipLaunchKernelGGL((k_lsv_spmv<true, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
-    else if (canon) hipLaunchKernelGGL((k_lsv_spmv<false, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
-    else if (halo) hipLaunchKernelGGL(k_lsv_spmv<true>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
-    else hipLaunchKernelGGL(k_lsv_spmv<false>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, stop_col, col);
+    if (canon && halo) hipLaunchKernelGGL((k_lsv_spmv<true, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, xord, stop_col, col);
+    else if (canon) hipLaunchKernelGGL((k_lsv_spmv<false, true>), dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, xord, stop_col, col);
+    else if (halo) hipLaunchKernelGGL(k_lsv_spmv<true>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, xord, stop_col, col);
+    else hipLaunchKernelGGL(k_lsv_spmv<false>, dim3((unsigned)g), dim3(NT), 0, s, pk, dict, lsv, x, halo, y, (int)n, L, lblk, xord, stop_col, col);
     return hipGetLastError();
 }
 

@@ -16,34 +16,44 @@ namespace vtk {
 // the diagonal (2), stored in ascending column order.  The columns of x -+ 1 in local numbering:
 // one rank periodic ((x -+ 1) mod X) L + v; across ranks the first / last line's outer
 // neighbour is a halo line (n + block L + v).  VM, D, VP are always in that order; the x
-// couplings sort before them ("small") or after them, the two among themselves by column --
-// the same for every v of a line.  Returns the 5 kinds in stored order, 3 bits each.
+// couplings sort before them ("small") or after them by their GLOBAL column (the stored CSR
+// order): locally numbered lines by position; across ranks the left halo line before the row
+// (a lower rank's line) and the right one after it, except where the slab starts at global line
+// 0 (xord bit 0: its left neighbour is the last line, after the row) or ends at the last line
+// (bit 1: its right neighbour is line 0, before the row).  Two couplings on the same side sort
+// x + 1 first (one rank: the wrapped line; across ranks: the lower global line).  The same for
+// every v of a line.  Returns the 5 kinds in stored order, 3 bits each.
 __device__ __forceinline__ int canon_order_xv(int64_t x, int64_t v, int64_t n, int L, int X, int lblk, int64_t &cxm,
-                                              int64_t &cxp) {
+                                              int64_t &cxp, int xord = 0) {
     const int64_t r = x * L + v;
+    bool ms, ps;   // "small": stored before the line's own entries
     if (lblk < 0) {   // (x -+ 1) mod X for 0 <= x < X, by selects (no 64-bit division)
         cxm = (x == 0 ? X - 1 : x - 1) * L + v;
         cxp = (x == X - 1 ? 0 : x + 1) * L + v;
+        ms = cxm < r;
+        ps = cxp < r;
     } else {
         cxm = x >= 1 ? r - L : n + (int64_t)lblk * L + v;
         cxp = x <= X - 2 ? r + L : n + (int64_t)(1 - lblk) * L + v;
+        ms = x >= 1 || !(xord & 1);
+        ps = x == X - 1 && (xord & 2);
     }
     int ord = 0, k = 0;
     auto put = [&](int kind) { ord |= kind << (3 * k++); };
-    const bool ms = cxm < r, ps = cxp < r;   // "small": before the line's own entries
-    if (ms && ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
+    if (ms && ps) { put(4); put(0); }
     else if (ms) put(0);
     else if (ps) put(4);
     put(1);
     put(2);
     put(3);
-    if (!ms && !ps) { put(cxm < cxp ? 0 : 4); put(cxm < cxp ? 4 : 0); }
+    if (!ms && !ps) { put(4); put(0); }
     else if (!ms) put(0);
     else if (!ps) put(4);
     return ord;
 }
-__device__ __forceinline__ int canon_order(int64_t r, int64_t n, int L, int X, int lblk, int64_t &cxm, int64_t &cxp) {
-    return canon_order_xv(r / L, r % L, n, L, X, lblk, cxm, cxp);
+__device__ __forceinline__ int canon_order(int64_t r, int64_t n, int L, int X, int lblk, int64_t &cxm, int64_t &cxp,
+                                           int xord = 0) {
+    return canon_order_xv(r / L, r % L, n, L, X, lblk, cxm, cxp, xord);
 }
 
 // the entries of canonical row (xl, v) -- row = xl L + v, local numbering, n local rows, X = n / L
@@ -52,10 +62,10 @@ __device__ __forceinline__ int canon_order(int64_t r, int64_t n, int L, int X, i
 // The SELL copy of the same row holds the same columns and values in the same order, padding
 // after them, so a sum over these in order equals the SELL sum bit for bit
 __device__ __forceinline__ void canon_row(const double *__restrict__ lsv, int n, int L, int lblk, int xl, int v,
-                                          double drow, int (&c)[5], double (&d)[5]) {
+                                          double drow, int (&c)[5], double (&d)[5], int xord = 0) {
     const int X = n / L, row = xl * L + v;
     int64_t cxm, cxp;
-    const int ord = canon_order_xv(xl, v, n, L, X, lblk, cxm, cxp);
+    const int ord = canon_order_xv(xl, v, n, L, X, lblk, cxm, cxp, xord);
 #pragma unroll
     for (int e = 0; e < 5; ++e) {
         const int kind = (ord >> (3 * e)) & 7;

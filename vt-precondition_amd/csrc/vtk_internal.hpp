@@ -270,6 +270,7 @@ struct vtk_csr {
     // the per-step ghost exchange (BAND_GHOST_VECS L doubles per side), -1 offsets: no such side
     bool band_ghost = false;                            // band across ranks: per-step ghost exchange
     int band_lblk = 0;
+    int band_xord = 0;                                  // bit 0: slab starts at global line 0, bit 1: ends at the last line
     int band_peer[2] = {-1, -1};                        // left, right neighbour rank
     std::vector<int64_t> band_scnt, band_soff, band_rcnt, band_roff;
     int64_t band_off_first = -1, band_off_last = -1;    // send offsets of the first / last line
@@ -314,6 +315,7 @@ struct SpmvIn {
     // line-separable values (SELL, f64; solver launches only -- vtk_spmv keeps the SELL values)
     const double *lsv = nullptr;
     int lsv_L = 0, lsv_lblk = -1;
+    int lsv_xord = 0;    // across ranks: the halo lines' place in the stored order (vtk_csr::band_xord)
     int lsv_canon = 0;   // ... and every row canonical: k_sell computes the columns (canon_row)
     int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX; vtk::Tuning)
     Grid4 g4{};          // 4D grid rows (solver launches; g4.tab null: not used)
@@ -474,6 +476,7 @@ struct BandK {
                                  // v_k (k < j) and w_j, w_{j-1} by parity in slots m, m+1
                                  // (k_ghost_unpack); null on one rank
     int left_blk;                // halo block (0 / 1) holding the left neighbour line
+    int xord = 0;                // bit 0: the slab starts at global line 0, bit 1: ends at the last line
     const double *lsv;           // line-separable values (vtk_csr::d_lsv) or null: SELL values
     int canon;                   // with lsv: canonical rows (vtk_csr::lsv_canon), no codes read;
                                  // 2: the SpMV as straight-line code per line order
@@ -503,7 +506,7 @@ int band_parts(int64_t L, int lp = BAND_LP);   // parts per line (rows per part 
 // some entry is not reproduced bit-exactly (or is no diagonal / v+-1 / same-position x+-1
 // coupling).  lblk < 0: one rank (x couplings periodic); else the halo block of the left line
 hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const double *data, int64_t n, int L,
-                            int lblk, double *lsv, int *bad, hipStream_t s);
+                            int lblk, int xord, double *lsv, int *bad, hipStream_t s);
 // y = A x from the line-separable tables and the SELL codes (uniform width 5, coded columns):
 // k_sell's plain SpMV, the same bits.  halo != null: the distributed layout (lblk the left block)
 // the x-line ring SpMV with the solver's epilogues (one rank, canonical rows; k_lsv_ring_epi):
@@ -516,7 +519,7 @@ hipError_t launch_lsv_ring_epi(int epi, const double *lsv, const double *x, cons
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
                            hipStream_t s, int canon, int grid_cap,
-                           int ring_wgs = 0);   // canon: rows canonical, no codes read; ring_wgs > 0: LDS-staged x
+                           int ring_wgs = 0, int xord = 0);   // canon: rows canonical, no codes read; ring_wgs > 0: LDS-staged x
                                                 // (k_lsv_ring, about that many workgroups; one rank, canon)
 // 4D grid tables (vtk::Grid4) from the CSR (pass 0) and the check (pass 1): *bad |= 1 when an entry
 // is no grid coupling or differs from its table value, |= 2 when a row is not in ascending

@@ -64,6 +64,7 @@ struct SpmvK {
     // entry's value from its column -- the same value, so the same sums
     const double *lsv;
     int lsv_L, lsv_lblk;
+    int lsv_xord;   // across ranks: where the halo lines sort in the stored order (canon_order_xv)
     int canon;   // with lsv: every row canonical (vtk_csr::lsv_canon): columns from canon_row
     int swz;     // XCD-aware group order (xcd_swizzle; vtk::Tuning::sell_swz)
     Grid4 g4;    // 4D grid rows: columns from the coordinates, values from D / tables (g4.tab null: off)
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 int c[5];
                 double d[5];
                 if (act) {
-                    canon_row(a.lsv, a.n_local, L, a.lsv_lblk, xl, v, __builtin_nontemporal_load(a.lsv + row), c, d);
+                    canon_row(a.lsv, a.n_local, L, a.lsv_lblk, xl, v, __builtin_nontemporal_load(a.lsv + row), c, d, a.lsv_xord);
                 } else {
 #pragma unroll
                     for (int u = 0; u < 5; ++u) {
@@ -1131,7 +1132,7 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0,
                       sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
                       sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0,
-                      sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk,
+                      sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk, in.lsv_xord,
                       sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0, in.swz,
                       sell ? in.g4 : Grid4{}};
     return a;
