@@ -309,6 +309,17 @@ Red reduce(vtk_ctx *c, double *part, int cnt, int &rc) {
     return Red{part, cnt};
 }
 
+// across ranks the all-reduced partial vectors must have one length on every rank: a reducing
+// launch whose grid follows the slab (the 4D and x-line rings) zero-pads its partials to GMAX, as
+// every other reducing launch runs GMAX workgroups there (grid_for)
+int pad_partials(vtk_ctx *c, double *p0, double *p1, int &g) {
+    if (!c->dist || g >= GMAX) return VTK_OK;
+    for (double *p : {p0, p1})
+        if (p) HIPCHK(c, hipMemsetAsync(p + g, 0, (size_t)(GMAX - g) * sizeof(double), c->stream));
+    g = GMAX;
+    return VTK_OK;
+}
+
 int halo_exchange(vtk_csr *A, const double *x) {
     vtk_ctx *c = A->ctx;
     // no peer of this rank: RCCL point-to-point needs no call; the host-staged alltoallv is a
@@ -1053,9 +1064,13 @@ struct Solver {
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
 // the x-line ring with the solver's epilogues (k_lsv_ring_epi): one rank, line-separable canonical
 // rows, their tables in use (tunings band_lsv, sell_canon), the tridiagonal BJ(8) when bj
+// (across ranks: the slab's x-halo lines come from the two neighbour lines of the halo -- band_ghost --
+// or, on a rank without neighbours, the one-rank wrap)
 bool cyc_ring_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M, bool bj) {
-    if (c->tune.cyc_ring <= 0 || c->dist || !A->d_lsv || !A->lsv_canon || A->band_L <= 0 || A->band_L % 8 != 0 ||
-        !c->tune.band_lsv || !c->tune.sell_canon || band_parts(A->band_L) < 1 || A->n_local / A->band_L < 3)
+    const bool solo = !c->dist || (A->n_halo == 0 && A->n_send == 0 && !A->band_ghost);
+    if (c->tune.cyc_ring <= 0 || (!solo && !A->band_ghost) || !A->d_lsv || !A->lsv_canon || A->band_L <= 0 ||
+        A->band_L % 8 != 0 || !c->tune.band_lsv || !c->tune.sell_canon || band_parts(A->band_L) < 1 ||
+        A->n_local / A->band_L < (A->band_ghost ? 2 : 3))
         return false;
     if (!bj) return true;
     return M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr;
@@ -1199,6 +1214,15 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *w_cur = band ? wb[j % 3] : s.w;
         if (band && j > 0) {
             cnt = s.band_grid(j - 1, s.ghost ? 0 : c->tune.band_opt, c->tune.band_j3);
+        } else if (fused && band && j == 0 && cyc_ring_ok(c, s.A, s.M, true)) {
+            // step 0 of a band cycle through the x-line ring (x = v_0; the j = 0 dots only);
+            // across ranks the two halo lines first (12.8 KB at C3)
+            TRY(halo_exchange(s.A, pj));
+            Prof pf(c, "spmv_bj_dc", j, b_step);
+            const bool hl = s.A->band_ghost;
+            HIPCHK(c, launch_lsv_ring_epi(EPI_PREC_DC, s.A->d_lsv, pj, nullptr, s.M->d_tri + s.M->tri_ld, s.w, nullptr,
+                                          nullptr, s.dcpart, n, (int)s.A->band_L, c->tune.cyc_ring, stop, j, &cnt,
+                                          c->stream, hl ? s.A->d_halo : nullptr, s.A->band_lblk, s.A->band_xord));
         } else if (fused && bj_split(s.M)) {
             // interior tiles while the halo is in flight, boundary tiles once it has landed;
             // their partials side by side (cnt = both grids)
@@ -1225,12 +1249,6 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                          c->stream));
                 cnt += spmv_grid(bd);
             }
-        } else if (fused && band && j == 0 && cyc_ring_ok(c, s.A, s.M, true)) {
-            // step 0 of a band cycle through the x-line ring (x = v_0; the j = 0 dots only)
-            Prof pf(c, "spmv_bj_dc", j, b_step);
-            HIPCHK(c, launch_lsv_ring_epi(EPI_PREC_DC, s.A->d_lsv, pj, nullptr, s.M->d_tri + s.M->tri_ld, s.w, nullptr,
-                                          nullptr, s.dcpart, n, (int)s.A->band_L, c->tune.cyc_ring, stop, j, &cnt,
-                                          c->stream));
         } else if (fused) {
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
@@ -1597,13 +1615,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             HIPCHK(c, launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
                                      c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, &dd, &g, nullptr,
                                      0, c->stream));
-            // across ranks the all-reduced partial vectors must have one length on every rank
-            // (the ring's grid follows the slab): zero-pad to GMAX, as every other reducing launch
-            if (c->dist && g < GMAX) {
-                HIPCHK(c, hipMemsetAsync(prr + g, 0, (size_t)(GMAX - g) * sizeof(double), c->stream));
-                HIPCHK(c, hipMemsetAsync(prz + g, 0, (size_t)(GMAX - g) * sizeof(double), c->stream));
-                g = GMAX;
-            }
+            TRY(pad_partials(c, prr, prz, g));
             rr = reduce(c, prr, g, rc2);
             TRY(rc2);
             rz = reduce(c, prz, g, rc2);
@@ -1612,7 +1624,9 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
             int g = 0;
             HIPCHK(c, launch_lsv_ring_epi(EPI_RESID_PREC, A->d_lsv, x, b, M->d_tri + M->tri_ld, s.V, prr, prz, nullptr,
-                                          n, (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream));
+                                          n, (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream,
+                                          A->band_ghost ? A->d_halo : nullptr, A->band_lblk, A->band_xord));
+            TRY(pad_partials(c, prr, prz, g));
             rr = reduce(c, prr, g, rc2);
             TRY(rc2);
             rz = reduce(c, prz, g, rc2);
@@ -1629,7 +1643,9 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             Prof pf(c, "spmv_resid", -1, solver_matrix_bytes(A) + 3 * n8);
             int g = 0;
             HIPCHK(c, launch_lsv_ring_epi(EPI_RESID, A->d_lsv, x, b, nullptr, s.r, prr, nullptr, nullptr, n,
-                                          (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream));
+                                          (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream,
+                                          A->band_ghost ? A->d_halo : nullptr, A->band_lblk, A->band_xord));
+            TRY(pad_partials(c, prr, nullptr, g));
             rr = reduce(c, prr, g, rc2);
             TRY(rc2);
         } else {

@@ -1325,12 +1325,16 @@ hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s) {
 // with M^-1 the tridiagonal BJ(8) of bj_trim_group (the same operations as k_sell's TRIM
 // epilogue).  The reductions: per lane over its rows in line order, then wave_sum, then the
 // waves in order -- one partial per workgroup (PREC_DC: launch_dc_dots' layout).
+// halo (distributed, vtk_csr::band_ghost): the two neighbour lines (blocks lblk = left and
+// 1 - lblk = right of L doubles, after halo_exchange), xord their place in the stored order
 struct LsvEpiK {
     const double *lsv, *x, *b, *mtri;
     double *y, *p0, *p1, *dcpart;
     int n, L, H;
     const int *stop_col;
     int col;
+    const double *halo;
+    int lblk, xord;
 };
 template <int EPI>
 __global__ __launch_bounds__(BAND_T) void k_lsv_ring_epi(LsvEpiK a) {
@@ -1348,17 +1352,24 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring_epi(LsvEpiK a) {
     const bool own = tid >= 8 && tid < 8 + LP;
     const double tx0 = own ? lsv[n + v] : 0.0, tx1 = own ? lsv[n + L + v] : 0.0;
     auto line_of = [&](int it) { return it == 0 ? (xa == 0 ? X - 1 : xa - 1) : (it == nl + 1 ? (xb == X ? 0 : xb) : xa - 1 + it); };
+    // the rows of iteration it's line: x, or a neighbour rank's line (the slab's x-halo) in halo
+    const double *hal = a.halo;
+    auto line_ptr = [&](int it) -> const double * {
+        if (hal && it == 0 && xa == 0) return hal + (int64_t)a.lblk * L;
+        if (hal && it == nl + 1 && xb == X) return hal + (int64_t)(1 - a.lblk) * L;
+        return x + (int64_t)line_of(it) * L;
+    };
     auto slot = [&](int it) { return (it & 3) * BAND_T; };
     constexpr bool BJ = EPI == EPI_RESID_PREC || EPI == EPI_PREC_DC;
     constexpr bool HB = EPI == EPI_RESID || EPI == EPI_RESID_PREC;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     // prefetch: x of line_of(it), and D (m, b) of line it - 1 (computed at iteration it)
-    double nxv = inl ? __builtin_nontemporal_load(x + (int64_t)line_of(0) * L + v) : 0.0, nd = 0.0, nm = 1.0, nb = 0.0;
+    double nxv = inl ? __builtin_nontemporal_load(line_ptr(0) + v) : 0.0, nd = 0.0, nm = 1.0, nb = 0.0;
     for (int it = 0; it <= nl + 1; ++it) {
         ring[slot(it) + tid] = nxv;
         const double drow = nd, mrow = nm, brow = nb;
         if (it <= nl) {
-            nxv = inl ? __builtin_nontemporal_load(x + (int64_t)line_of(it + 1) * L + v) : 0.0;
+            nxv = inl ? __builtin_nontemporal_load(line_ptr(it + 1) + v) : 0.0;
             if (own && it + 1 >= 2) {
                 const int64_t rr = (int64_t)(xa + it - 1) * L + v;
                 nd = __builtin_nontemporal_load(lsv + rr);
@@ -1371,7 +1382,7 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring_epi(LsvEpiK a) {
             const int xl = xa + it - 2;
             const double tv0 = lsv[n + 2 * L + xl], tv1 = lsv[n + 2 * L + X + xl];
             int64_t cxm, cxp;
-            const int ord = __builtin_amdgcn_readfirstlane(canon_order_xv(xl, 0, n, L, X, -1, cxm, cxp));
+            const int ord = __builtin_amdgcn_readfirstlane(canon_order_xv(xl, 0, n, L, X, hal ? a.lblk : -1, cxm, cxp, a.xord));
             constexpr int P_MID = 0 | 1 << 3 | 2 << 6 | 3 << 9 | 4 << 12;
             constexpr int P_FIRST = 1 | 2 << 3 | 3 << 6 | 4 << 9 | 0 << 12;
             const int sx = slot(it - 1);
@@ -1446,17 +1457,20 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring_epi(LsvEpiK a) {
 
 hipError_t launch_lsv_ring_epi(int epi, const double *lsv, const double *x, const double *b, const double *mtri,
                                double *y, double *p0, double *p1, double *dcpart, int64_t n, int L, int ring_wgs,
-                               const int *stop_col, int col, int *grid_out, hipStream_t s) {
+                               const int *stop_col, int col, int *grid_out, hipStream_t s, const double *halo, int lblk,
+                               int xord) {
     const int H = band_parts(L);
     const int64_t X = L > 0 ? n / L : 0;
-    if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || H < 1 || X < 3 || ring_wgs < 1) return hipErrorInvalidValue;
+    if (n <= 0 || n > INT32_MAX / 2 || L <= 0 || n % L != 0 || H < 1 || X < (halo ? 2 : 3) || ring_wgs < 1 ||
+        (halo && (lblk < 0 || lblk > 1)))
+        return hipErrorInvalidValue;
     const bool bj = epi == EPI_RESID_PREC || epi == EPI_PREC_DC;
     if ((bj && !mtri) || ((epi == EPI_RESID || epi == EPI_RESID_PREC) && (!b || !p0)) ||
         (epi == EPI_RESID_PREC && !p1) || (epi == EPI_PREC_DC && !dcpart) || L % 8 != 0)
         return hipErrorInvalidValue;
     // one partial per workgroup: at most GMAX
     const int64_t R = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ring_wgs / H, X / 2), GMAX / H));
-    LsvEpiK a{lsv, x, b, mtri, y, p0, p1, dcpart, (int)n, L, H, stop_col, col};
+    LsvEpiK a{lsv, x, b, mtri, y, p0, p1, dcpart, (int)n, L, H, stop_col, col, halo, halo ? lblk : -1, halo ? xord : 0};
     const dim3 g((unsigned)(R * H)), blk(BAND_T);
     if (grid_out) *grid_out = (int)g.x;
     switch (epi) {

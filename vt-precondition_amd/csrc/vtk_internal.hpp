@@ -515,7 +515,8 @@ hipError_t launch_lsv_build(const int32_t *indptr, const int32_t *indices, const
 // *grid_out partials (<= GMAX)
 hipError_t launch_lsv_ring_epi(int epi, const double *lsv, const double *x, const double *b, const double *mtri,
                                double *y, double *p0, double *p1, double *dcpart, int64_t n, int L, int ring_wgs,
-                               const int *stop_col, int col, int *grid_out, hipStream_t s);
+                               const int *stop_col, int col, int *grid_out, hipStream_t s, const double *halo = nullptr,
+                               int lblk = -1, int xord = 0);   // halo: across ranks, the two neighbour lines
 hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double *lsv, const double *x,
                            const double *halo, double *y, int64_t n, int L, int lblk, const int *stop_col, int col,
                            hipStream_t s, int canon, int grid_cap,
