@@ -169,11 +169,10 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
  * settings exist for in-process A/B measurements and for the bit-identity tests (the same sums
  * with and without a byte-saving form).  Each key is seeded from the environment variable
  * VTK_<KEY in upper case> once, when the context is created; the library reads its environment
- * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_canon_sl, sell_pad,
- * sell_grid, plain_grid, sell_swz, plain_var, band_opt, band_j3, lsv_spmv_cap, lsv_ring,
- * line_sweep, ev_every, prof_perj, debug_band, comm_solo, auto_band, grid4, c4_fused, g4_ring,
- * g4_pd, g4_xcd, g4_dc, g4_gr, upd_grid, upd_xb, cyc_ring, g4_dc0, g4_res.
- * VTK_ERR_ARG for an unknown key.  (ABI 5) */
+ * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_opt, lsv_ring, prof_perj,
+ * comm_solo, auto_band, grid4, c4_fused, g4_ring, g4_gr, cyc_ring.
+ * VTK_ERR_ARG for an unknown key; a VTK_<KEY> variable of a key removed in round 5 draws a
+ * warning on stderr at context creation and is otherwise ignored.  (ABI 5) */
 int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);
 int vtk_ctx_get_tuning(vtk_ctx *ctx, const char *key, int *value);
 /* rank 0 creates the 128-byte RCCL unique id; the caller broadcasts it (any transport) */

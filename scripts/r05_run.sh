@@ -14,5 +14,9 @@ gpu) run t_gpu 1100 $T tests -m gpu ;;
 smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
 ab) run ab_${AB_ENV} 600 python tools/ab_env.py --env "$AB_ENV" --values "${AB_VALUES:-1,0}" --rounds "${AB_ROUNDS:-4}" --config "${AB_CFG:-C3}" --set "${AB_SET:-}" --perj ;;
 bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+slabs) for cp in C3:8 C3:4 C3:2 C4:8; do c=${cp%%:*}; p=${cp##*:}
+         run slab_${c}_$p 300 python bench.py --config $c --slab $p --comm-solo --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 2
+         grep '^{' gpurun_out/slab_${c}_$p.log | tail -1 >> gpurun_out/slabs.jsonl; done ;;
+c4) run bench_c4 600 python bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline ;;
 *) echo "unknown stage $st"; exit 2 ;;
 esac; done

@@ -179,31 +179,24 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
                 x2, i2, s2 = _solve(vk_lib, A, M, b, orth=orth)
             assert i1 == i0 == i2 == 0 and s1.inner_iters == s0.inner_iters
             assert np.array_equal(x1, x0), "grid rows change the bits"
-            # the split step's SpMV + BJ with x staged through LDS, operands 1..4 groups ahead
-            # (and 512-row groups)
-            for wgs, pd, gr in ((1, 3, 256), (3, 1, 256), (4096, 2, 256), (7, 4, 256), (1, 1, 512), (5, 1, 512)):
-                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_pd=pd, g4_gr=gr, g4_dc0=0, g4_res=0):
+            # the split step's SpMV + BJ with x staged through LDS (k_g4_ring), in 256- and 512-row
+            # groups over 1 .. 4096 workgroups, step 0's dots and the cycle-start residual in the
+            # ring kernel: its partials follow the workgroups (reductions in another fixed order:
+            # the solver bars; deterministic per setting)
+            for wgs, gr in ((1, 256), (3, 256), (4096, 256), (7, 256), (1, 512), (5, 512)):
+                with gpu.tuning(c4_fused=0, g4_ring=wgs, g4_gr=gr):
                     x3, i3, s3 = _solve(vk_lib, A, M, b, orth=orth)
-                assert i3 == 0 and s3.inner_iters == s1.inner_iters
-                assert np.array_equal(x1, x3), ("k_g4_ring changes the bits", wgs, pd, gr)
-            # default: the ring split step, step 0's dots and the cycle-start residual in the ring
-            # kernel (reductions in another fixed order: the solver bars; deterministic)
+                    x3b, _, s3b = _solve(vk_lib, A, M, b, orth=orth)
+                assert i3 == 0 and np.array_equal(x3, x3b) and s3.inner_iters == s3b.inner_iters, (wgs, gr)
+                assert abs(s3.inner_iters - s1.inner_iters) <= 1, (wgs, gr)
+                assert np.linalg.norm(x3 - x1) / np.linalg.norm(x1) < 1e-9, (wgs, gr)
+            # default: the ring split step (2048 workgroups of 512 rows)
             xd, _, sd = _solve(vk_lib, A, M, b, orth=orth)
             xe, _, se = _solve(vk_lib, A, M, b, orth=orth, x0=b * 1e-3)
             xf, _, sf = _solve(vk_lib, A, M, b, orth=orth, x0=b * 1e-3)
             assert np.array_equal(xe, xf) and se.inner_iters == sf.inner_iters
             assert abs(sd.inner_iters - s1.inner_iters) <= 1
             assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) < 1e-9
-            # the ring with the step's dots fused in: the dots sum in another fixed order
-            with gpu.tuning(g4_ring=2048, g4_dc=1, g4_res=0):
-                x4, i4, s4 = _solve(vk_lib, A, M, b, orth=orth)
-                x5, _, _ = _solve(vk_lib, A, M, b, orth=orth)
-            assert i4 == 0 and np.array_equal(x4, x5)
-            if orth == "mgs":
-                assert np.array_equal(x1, x4)
-            else:
-                assert abs(s4.inner_iters - s1.inner_iters) <= 1
-                assert np.linalg.norm(x4 - x1) / np.linalg.norm(x1) < 1e-9
             if orth == "mgs":
                 assert np.array_equal(x1, x2)
             else:   # the fused dots sum in another fixed order: the DCGS2 bars

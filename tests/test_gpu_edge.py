@@ -109,3 +109,25 @@ def test_device_csr_spare_capacity_and_stream(gpu, vk_lib):
     assert np.array_equal(A @ x, coracle.spmv(ip, ix, d32, x))
     with pytest.raises(TypeError):
         vk.csr_matrix((td, tix, tip.to("cpu")), shape=(n, n), ctx=gpu)
+
+
+def test_retired_tuning_env_warns():
+    """A VTK_<KEY> variable of a tuning switch removed in round 5 (vtk_api.cpp RETIRED_KEYS) is not
+    silently ignored: context creation names every such variable on stderr once; the switch is
+    gone from the key table (vtk_ctx_set_tuning -> VTK_ERR_ARG)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import vtkrylov as vk\n"
+            "c = vk.Context(0)\n"
+            "print(vk._abi.lib().vtk_ctx_set_tuning(c._h, b'g4_pd', 2))\n") % (
+        root, os.path.join(root, "vt-precondition_amd"))
+    env = dict(os.environ, VTK_G4_PD="2", VTK_UPD_XB="8")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "VTK_G4_PD is set but no longer has an effect" in r.stderr
+    assert "VTK_UPD_XB is set but no longer has an effect" in r.stderr
+    import vtkrylov as vk
+    assert int(r.stdout.strip().splitlines()[-1]) == vk._abi.ERR_ARG

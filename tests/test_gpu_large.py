@@ -71,9 +71,9 @@ def test_gmres_full_size_vs_scipy(gpu, vk_lib, golden_large, name, path):
 @pytest.mark.parametrize("path", sorted(PATHS))
 def test_gmres_c4_vs_scipy(gpu, vk_lib, golden_large, path):
     g = golden_large["C4"].get("gmres_bj8")
-    assert g["source"].startswith("scipy.sparse.linalg.gmres")
     if g is None:
         pytest.fail("golden_large.json has no C4 summary (make_golden.py --gmres-large C4)")
+    assert g["source"].startswith("scipy.sparse.linalg.gmres")
     p, x, info, st, b, csr, layout, mmode = _solve(vk_lib, gpu, "C4", path)
     assert layout == "sell"
     _check(g, x, info, st, b, csr)

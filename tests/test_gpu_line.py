@@ -324,17 +324,5 @@ def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
             x3, i3 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
         assert i3 == 0 and it1 == vk_lib.last_stats().inner_iters
         assert np.array_equal(x1, x3), wgs
-    # the update pass fused with the next table SpMV (k_line_sweep): k_dc_update's and the table
-    # SpMV's operations, p kept apart from V -- bit-identical, also with a non-zero x0, restart 5
-    # (several cycles, x updates inside the sweep) and 1-line ranges
-    x0 = twin.rhs(p.n, seed=0xB0B) * 1e-3
-    for kw in ({}, {"x0": x0}, {"restart": 5}):
-        xr, ir = vk_lib.gmres(A, b, rtol=1e-8, M=M, **kw)
-        itr = vk_lib.last_stats().inner_iters
-        for wgs in (4096, 64):
-            with gpu.tuning(line_sweep=wgs):
-                xs, i_s = vk_lib.gmres(A, b, rtol=1e-8, M=M, **kw)
-            assert i_s == ir == 0 and itr == vk_lib.last_stats().inner_iters, (kw, wgs)
-            assert np.array_equal(xr, xs), (kw, wgs)
     M.close()
     A.close()

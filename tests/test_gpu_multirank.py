@@ -38,9 +38,8 @@ def _worker(rank, world, port, case, outdir, from_host, orth):
     planes = isinstance(from_host, str) and from_host.startswith("planes")
     if planes:   # slabs of whole x planes: the 4D grid rows hold across ranks (halo planes)
         align = p.shape[1] * p.shape[2] * p.shape[3]
-        if from_host == "planes_ring":   # the LDS-ring step with the dots fused, across ranks
+        if from_host == "planes_ring":   # the LDS-ring step across ranks, 64 workgroups
             ctx.set_tuning("g4_ring", 64)
-            ctx.set_tuning("g4_dc", 1)
         elif from_host.startswith("planes_ring512"):   # ... and in 512-row groups, dots apart
             ctx.set_tuning("g4_ring", 2)
             ctx.set_tuning("g4_gr", 512)

@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--slab", type=int, default=1, help="one rank's x-slab at this many GPUs (as bench.py --slab)")
     ap.add_argument("--comm-solo", action="store_true", help="the distributed code path on one rank (bench.py --comm-solo)")
     ap.add_argument("--perj", action="store_true", help="also one profiled solve per value: band step us per j")
-    ap.add_argument("--set", default="", help="fixed tuning for every value, e.g. band_j3=4,sell_swz=1")
+    ap.add_argument("--set", default="", help="fixed tuning for every value, e.g. band_opt=1,lsv_ring=0")
     a = ap.parse_args()
     import vtkrylov as vk
     from oracle import twin
@@ -77,7 +77,7 @@ def main():
             ctx.profile(False)
             perj[v] = {k: round(e["avg_us"], 1) for k, e in sorted(pr.items())
                        if k.startswith("band_step") or k in ("dc_scalar", "dc_update", "spmv_resid_bj", "spmv_bj_dc",
-                                                             "line_sweep", "line_dc", "spmv_lsv", "xupdate", "spmv_bj",
+                                                             "line_dc", "spmv_lsv", "xupdate", "spmv_bj",
                                                              "dc_dots", "spmv_resid")}
         ctx.set_tuning("prof_perj", 0)
     out = {"config": a.config, "set": a.set, "perj_us": perj, "prec": a.prec, "slab": a.slab, "comm_solo": a.comm_solo, "env": a.env, "iters_band_info": iters,

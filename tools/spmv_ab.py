@@ -1,7 +1,7 @@
 """In-process A/B of the plain SpMV (vtk_spmv, the measured half of the metric) over context
 tuning settings: one operator, alternating settings, HIP-event timing on the library's stream.
 
-    python tools/spmv_ab.py --config C3 --settings "sell_swz=0;sell_swz=1;sell_swz=1,plain_grid=4096"
+    python tools/spmv_ab.py --config C3 --settings "sell_canon=0;sell_canon=1;grid4=0"
 
 Prints one JSON line: per setting the per-launch microseconds of every round and their median,
 and the algorithmic GB/s (layout bytes + x + y)."""
@@ -21,7 +21,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "vt-precondition_amd")]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--settings", default="sell_swz=0;sell_swz=1")
+    ap.add_argument("--settings", default="sell_canon=0;sell_canon=1")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=50)
     a = ap.parse_args()

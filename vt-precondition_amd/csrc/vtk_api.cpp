@@ -78,12 +78,17 @@ int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
 struct TuneKey { const char *name; int Tuning::*mem; };
 constexpr TuneKey TUNE_KEYS[] = {
     {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
-    {"band_canon", &Tuning::band_canon}, {"band_canon_sl", &Tuning::band_canon_sl},
-    {"sell_pad", &Tuning::sell_pad}, {"sell_grid", &Tuning::sell_grid}, {"plain_grid", &Tuning::plain_grid}, {"sell_swz", &Tuning::sell_swz}, {"plain_var", &Tuning::plain_var}, {"band_opt", &Tuning::band_opt}, {"band_j3", &Tuning::band_j3},
-    {"lsv_spmv_cap", &Tuning::lsv_spmv_cap}, {"lsv_ring", &Tuning::lsv_ring}, {"line_sweep", &Tuning::line_sweep}, {"ev_every", &Tuning::ev_every}, {"prof_perj", &Tuning::prof_perj},
-    {"debug_band", &Tuning::debug_band}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
-    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring}, {"g4_pd", &Tuning::g4_pd}, {"g4_xcd", &Tuning::g4_xcd}, {"g4_dc", &Tuning::g4_dc}, {"g4_gr", &Tuning::g4_gr}, {"upd_grid", &Tuning::upd_grid}, {"cyc_ring", &Tuning::cyc_ring}, {"g4_dc0", &Tuning::g4_dc0}, {"g4_res", &Tuning::g4_res}, {"upd_xb", &Tuning::upd_xb},
+    {"band_canon", &Tuning::band_canon}, {"band_opt", &Tuning::band_opt}, {"lsv_ring", &Tuning::lsv_ring},
+    {"prof_perj", &Tuning::prof_perj}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
+    {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring},
+    {"g4_gr", &Tuning::g4_gr}, {"cyc_ring", &Tuning::cyc_ring},
 };
+// switches of earlier rounds whose alternative lost its A/B: an environment that
+// still sets one is told once that it no longer has an effect
+constexpr const char *RETIRED_KEYS[] = {"band_canon_sl", "sell_pad", "sell_grid", "plain_grid", "sell_swz", "plain_var",
+                                        "band_j3", "lsv_spmv_cap", "line_sweep", "ev_every", "debug_band", "g4_pd",
+                                        "g4_xcd", "g4_dc", "g4_dc0", "g4_res", "upd_grid", "upd_xb", "sell_nopad",
+                                        "sell_lsv"};
 
 const TuneKey *tune_key(const char *name) {
     if (!name) return nullptr;
@@ -92,12 +97,24 @@ const TuneKey *tune_key(const char *name) {
     return nullptr;
 }
 
+std::string env_name(const char *key) {
+    std::string var = "VTK_";
+    for (const char *p = key; *p; ++p) var += (char)std::toupper((unsigned char)*p);
+    return var;
+}
+
 void tune_from_env(Tuning &t) {
-    for (const auto &k : TUNE_KEYS) {
-        std::string var = "VTK_";
-        for (const char *p = k.name; *p; ++p) var += (char)std::toupper((unsigned char)*p);
-        if (const char *e = std::getenv(var.c_str()); e && *e) t.*k.mem = std::atoi(e);
+    for (const auto &k : TUNE_KEYS)
+        if (const char *e = std::getenv(env_name(k.name).c_str()); e && *e) t.*k.mem = std::atoi(e);
+    // (a renamed or removed switch must not be silently ignored)
+    static bool warned = false;   // once per process, every retired variable that is set
+    for (const char *k : RETIRED_KEYS) {
+        const std::string var = env_name(k);
+        if (!warned && std::getenv(var.c_str()))
+            std::fprintf(stderr, "vtkrylov: %s is set but no longer has an effect (retired tuning switch, DESIGN.md §3f)\n",
+                         var.c_str());
     }
+    warned = true;
 }
 
 // ---- kernel profile: HIP events around each launch on the context stream ------------------
@@ -351,11 +368,13 @@ SpmvIn spmv_in(vtk_csr *A, const Tiles *t, const double *x, const Groups *g = nu
         in.sell = &A->sell;
         in.groups = g ? g : &A->g_all;
     }
-    in.plain_grid = A->ctx->tune.plain_grid;
-    // (the 9-wide 4D rows' plain SpMV: 648 -> 730 us swizzled -- their x +- 1 planes are 250 000
-    // rows away, not in the XCD's window -- so blockIdx order there)
-    in.swz = A->ctx->tune.sell_swz & ((A->use_sell && A->sell.uniform_w > 8) ? ~1 : ~0);
-    in.plain_var = A->ctx->tune.plain_var;
+    in.plain_grid = 2048;   // (grid sweep, C3: 2048 best; 3072: 293 us; 4096-100 000: 256-265)
+    // the plain SpMV walks its groups in XCD-contiguous order (C3 PMC fetch 1.40 -> 1.07 GB per
+    // launch, time neutral) -- except on the 9-wide 4D rows (648 -> 730 us swizzled: their x +- 1
+    // planes are 250 000 rows away, not in the XCD's window); the reducing launches keep
+    // blockIdx order, so their partial sums keep their bits
+    in.swz = (A->use_sell && A->sell.uniform_w > 8) ? 0 : 1;
+    in.plain_var = 1;   // padding gathers branched in the plain SpMV (243.6 -> 221.3 us)
     return in;
 }
 
@@ -526,7 +545,7 @@ int build_sell(vtk_csr *A, bool only_if_compact, bool *built) {
     // entry narrower) are padded to the widest chunk when that costs <= 2 % more entries: every
     // chunk's offset is then 64 W q and the kernels take the compile-time-width path (no offset
     // loads at the head of each chunk)
-    if (nch > 0 && c->tune.sell_pad) {
+    if (nch > 0) {
         std::vector<int64_t> off((size_t)nch + 1);
         e = hipMemcpy(off.data(), sl.d_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost);
         if (e != hipSuccess) { drop(); return fail(c, VTK_ERR_HIP, std::string("SELL build: ") + hipGetErrorString(e)); }
@@ -617,8 +636,6 @@ int build_groups(vtk_csr *A) {
     const int ng = (int)((A->n_local + 255) / 256);
     A->g_all.count = ng;
     A->g_all.grid = grid_for(c, std::max(1, std::min(ng, GMAX)));
-    if (c->tune.sell_grid > 0 && !c->dist)   // tuning experiments
-        A->g_all.grid = std::max(1, std::min({ng, GMAX, c->tune.sell_grid}));
     if (c->dist && A->row_halo.size() == (size_t)A->n_local) {
         std::vector<int32_t> gi, gb;
         for (int g = 0; g < ng; ++g) {
@@ -796,10 +813,6 @@ int band_check_all(vtk_csr *A, int64_t L) {
     vtk_ctx *c = A->ctx;
     BandCheck chk;
     int rc = band_check(A, L, chk);
-    if (c->tune.debug_band)
-        std::fprintf(stderr, "[vtk band] rank %d/%d L=%lld n_local=%lld n_halo=%lld n_send=%lld local rc=%d vloc=%d ghost=%d\n",
-                     c->rank, c->world, (long long)L, (long long)A->n_local, (long long)A->n_halo, (long long)A->n_send, rc,
-                     (int)chk.vloc, (int)chk.ghost);
     // line-separable values (rank-local: the kernels read them or the SELL values, the same bits
     // either way): built into a scope-owned buffer and checked against the CSR bit for bit;
     // committed below together with the layout only once every rank has passed
@@ -1024,12 +1037,6 @@ int auto_line_band(vtk_csr *A) {
 
 // ---- GMRES -----------------------------------------------------------------------------------
 
-#ifndef VTK_DC_FUSED
-#define VTK_DC_FUSED 1   // DCGS2 dots inside the SpMV + BJ kernel (0: SpMV + BJ, then k_dc_dots)
-#endif
-#ifndef VTK_LINE_DC
-#define VTK_LINE_DC 1    // line path: DCGS2 dots inside the line-apply kernel (0: k_dc_dots after it)
-#endif
 
 struct Solver {
     vtk_csr *A;
@@ -1048,17 +1055,9 @@ struct Solver {
     int band_G = 0, band_H = 1;
     int band_G3 = 0;   // grid of the three-workgroups-per-CU launches (band_opt bit 1, j <= BAND_J3)
     // workgroups (= partials) of the band step launched at step j
-    int band_grid(int j, int opt, int j3) const {
-        return (opt & 2) && j <= std::min(j3, BAND_J3) && band_G3 > 0 ? band_G3 : band_G;
-    }
+    int band_grid(int j, int opt) const { return (opt & 2) && j <= BAND_J3 && band_G3 > 0 ? band_G3 : band_G; }
     double *w3 = nullptr;
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
-    // line path with the fused update + table SpMV (k_line_sweep): p_j in pbuf[j & 1] (V[0] at
-    // j = 0), never in V[j]; sweep_R line ranges
-    bool sweep = false;
-    int sweep_R = 0;
-    double *pbuf[2] = {nullptr, nullptr};
-    const double *p_of(int j) const { return sweep && j > 0 ? pbuf[j & 1] : V + (size_t)j * ld; }
 };
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
@@ -1076,13 +1075,13 @@ bool cyc_ring_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M, bool bj) {
     return M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr;
 }
 
-// the 4D grid rows' cycle-start residual through k_g4_ring (tunings g4_ring, g4_res; BJ(8) tridiag)
+// the 4D grid rows' cycle-start residual through k_g4_ring (tuning g4_ring; BJ(8) tridiag)
 // (only for grids whose window and tables fit the kernel's LDS, g4_ring_fits; larger 4D
 // grids keep the SELL grid-row kernels)
 bool g4_resid_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M) {
-    return A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && c->tune.g4_res && A->use_sell &&
+    return A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && A->use_sell &&
            A->sell.uniform_w > 8 && M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr &&
-           g4_ring_fits(A->g4, A->n_local, c->tune.g4_gr, 3);
+           g4_ring_fits(A->g4, A->n_local, c->tune.g4_gr);
 }
 
 int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0,
@@ -1138,19 +1137,18 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // there the SpMV + BJ kernel and the streaming dots kernel beat the register-capped fused
     // kernel (C4: 707 + 658 us vs 1473 us per step, 422 vs 405 it/s)
     // (with the 4D grid rows (Grid4) the fused kernel loads no values or codes: tuning c4_fused)
-    const bool g4_fits = s.A->d_g4tab && g4_ring_fits(s.A->g4, n, c->tune.g4_gr, 0);
+    const bool g4_fits = s.A->d_g4tab && g4_ring_fits(s.A->g4, n, c->tune.g4_gr);
     const bool g4_fused = s.A->d_g4tab && c->tune.grid4 && c->tune.c4_fused && (c->tune.g4_ring <= 0 || !g4_fits);   // C4 A/B: 213.8 -> 210.3 ms
     // grid rows with x staged through LDS (k_g4_ring) for the split step's SpMV + BJ
-    // (every mode the cycle launches fits when mode 0 fits: g4_ring_group)
     const bool g4_ring = s.A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && s.A->use_sell && s.M &&
                          s.M->kind == VTK_PREC_BJACOBI && s.M->bs == 8 && bj_op(s.M).tri != nullptr && g4_fits;
     const bool wide9 = s.A->use_sell && s.A->sell.uniform_w > 8 && !bj_split(s.M) && !g4_fused;
     // the ring step also across ranks: interior groups while the halo planes
     // are in flight, the boundary planes' groups once they have landed
     const bool ring4 = g4_ring && s.A->use_sell && s.A->sell.uniform_w > 8 && !g4_fused;
-    const bool fused = VTK_DC_FUSED && bj_fused(s.M) && s.M->bs <= 8 && !wide9 && !ring4;
+    const bool fused = bj_fused(s.M) && s.M->bs <= 8 && !wide9 && !ring4;
     // line Jacobi with segments <= 32 (register sweeps): dots fused into the sweep kernel
-    const bool line_dc = VTK_LINE_DC && s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
+    const bool line_dc = s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
                          s.M->line.seg <= 32 && s.G <= GMAX;
     // line path on a line-separable operator: the SpMV from the tables (VTK_BAND_LSV=0: SELL)
     const bool line_lsv = line_dc && s.A->d_lsv && s.A->band_L > 0 && c->tune.band_lsv && s.A->use_sell &&
@@ -1194,7 +1192,6 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // line-separable values in the band step (tuning band_lsv 0: the SELL values)
     const bool band_lsv = band && s.A->d_lsv && c->tune.band_lsv;
     const bool band_canon = c->tune.band_canon != 0;       // 0: read the codes anyway (A/B)
-    const bool canon_sl = c->tune.band_canon_sl != 0;      // 0: the per-entry loop (A/B)
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)
     const double b_band = band_lsv ? (s.A->lsv_canon && band_canon
@@ -1202,7 +1199,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                           : b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n)
                                    : b_csr;
     bool broke = false;
-    const int ev_every = c->tune.ev_every >= 1 && c->tune.ev_every <= LOOKAHEAD + 1 ? c->tune.ev_every : 1;
+    constexpr int ev_every = 1;   // (every 2 or 4 steps measured neutral)
     int ev_step[LOOKAHEAD + 1];
     int nev = 0, synced = 0;
     for (int j = 0; j < m; ++j) {
@@ -1213,7 +1210,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *const wb[3] = {s.w, s.tmp, s.w3};
         double *w_cur = band ? wb[j % 3] : s.w;
         if (band && j > 0) {
-            cnt = s.band_grid(j - 1, s.ghost ? 0 : c->tune.band_opt, c->tune.band_j3);
+            cnt = s.band_grid(j - 1, s.ghost ? 0 : c->tune.band_opt);
         } else if (fused && band && j == 0 && cyc_ring_ok(c, s.A, s.M, true)) {
             // step 0 of a band cycle through the x-line ring (x = v_0; the j = 0 dots only);
             // across ranks the two halo lines first (12.8 KB at C3)
@@ -1256,16 +1253,14 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             cnt = spmv_grid(in);
         } else if (line_dc) {
-            // line path: SpMV, then the line sweeps with the step's dots fused behind them (with
-            // the fused update + SpMV sweep, tmp = A p_j already came from step j-1's sweep)
+            // line path: SpMV, then the line sweeps with the step's dots fused behind them
             TRY(halo_exchange(s.A, pj));
-            if (s.sweep && j > 0) {
-            } else if (line_lsv) {
+            if (line_lsv) {
                 // line-separable values: 12 B of matrix per row (codes + diagonal)
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
                                           s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
-                                          c->stream, line_canon ? 1 : 0, c->tune.lsv_spmv_cap, c->tune.lsv_ring,
+                                          c->stream, line_canon ? 1 : 0, 8192, c->tune.lsv_ring,
                                           s.A->band_ghost ? s.A->band_xord : 0));
             } else {
                 Prof pf(c, "spmv", j, b_csr + 2 * n8);
@@ -1273,34 +1268,32 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                       nullptr, stop, j, c->stream));
             }
             { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
-              HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, s.p_of(j), s.dcpart, s.G, stop, j, c->stream)); }
+              HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream)); }
             cnt = s.G;
         } else if (ring4) {
-            // g4_dc: the step's dots in the same sweep (+ V_j; w is still written for the update)
+            // step 0's dots (|p|^2, p.w, |w|^2) in the same sweep; the later steps' dots in
+            // k_dc_dots (fused into the ring they cost 215.6 vs 201.5 ms per C4 solve: the ring
+            // then runs at 3 waves/SIMD and its basis reads wait behind the ring's)
             G4Dots dd;
-            dd.V = s.V;
-            dd.ld = s.ld;
-            dd.j = j;
             dd.part = s.dcpart;
-            // g4_dc: every step's dots fused in; step 0's (|p|^2, p.w, |w|^2 only) by default
-            const bool dc = c->tune.g4_dc != 0 || (j == 0 && c->tune.g4_dc0 != 0);
-            dd.mode = c->tune.g4_dc != 0 ? 1 : 2;
-            const double b_ring = solver_matrix_bytes(s.A) + b_inv + 2 * n8 + (dc ? n8 * j : 0.0);   // D, m, x, w (+ V_j)
+            const bool dc = j == 0;
+            dd.mode = 2;
+            const double b_ring = solver_matrix_bytes(s.A) + b_inv + 2 * n8;   // D, m, x, w
             const double *halo = s.A->g4.lblk >= 0 ? s.A->d_halo : nullptr;
             const double *mt = s.M->d_tri + s.M->tri_ld;
             if (!halo || !bj_split(s.M)) {
                 TRY(halo_exchange(s.A, pj));
                 Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring);
                 int grid = 0;
-                HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd,
-                                         c->tune.g4_xcd, c->tune.g4_gr, dc ? &dd : nullptr, &grid, stop, j, c->stream));
+                HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_gr,
+                                         dc ? &dd : nullptr, &grid, stop, j, c->stream));
                 if (dc) cnt = grid;
             } else {
                 // across ranks: the rows [S4, n - S4) read no halo plane -- their groups run while
                 // the exchange is in flight (comm stream), the first / last plane's groups after it
                 // lands; the partials of the three launches side by side
                 const int mode = dc ? dd.mode : 0;
-                const int G = g4_ring_group(c->tune.g4_gr, mode);
+                const int G = g4_ring_group(c->tune.g4_gr);
                 const int64_t S4 = (int64_t)s.A->g4.Ny * s.A->g4.Nvx * s.A->g4.Nvy, ng = (n + G - 1) / G;
                 int64_t gi_lo = (S4 + G - 1) / G, gi_hi = (n - S4) / G;
                 if (gi_hi <= gi_lo) gi_lo = gi_hi = 0;   // no interior group: all after the exchange
@@ -1312,7 +1305,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 {
                     Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring * (double)(gi_hi - gi_lo) * G / std::max<double>(1.0, (double)n));
                     if (gi_hi > gi_lo)
-                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, 0,
+                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                                  c->tune.g4_gr, dc ? &dd : nullptr, &gin, stop, j, c->stream, (int)gi_lo,
                                                  (int)gi_hi, per));
                 }
@@ -1320,12 +1313,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 {
                     Prof pf(c, "spmv_bj_bd", j, b_ring * std::max(0.0, 1.0 - (double)(gi_hi - gi_lo) * G / std::max<double>(1.0, (double)n)));
                     dd.part_off = gin;
-                    HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, 0,
+                    HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                              c->tune.g4_gr, dc ? &dd : nullptr, &gb0, stop, j, c->stream, 0,
                                              (int)(gi_hi > gi_lo ? gi_lo : ng), per));
                     if (gi_hi > gi_lo) {
                         dd.part_off = gin + gb0;
-                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_pd, 0,
+                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                                  c->tune.g4_gr, dc ? &dd : nullptr, &gb1, stop, j, c->stream, (int)gi_hi,
                                                  (int)ng, per));
                     }
@@ -1392,37 +1385,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.left_blk = s.A->band_lblk;
             a.xord = s.A->band_xord;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
-            a.canon = band_lsv && s.A->lsv_canon && band_canon ? (canon_sl ? 2 : 1) : 0;
+            a.canon = band_lsv && s.A->lsv_canon && band_canon ? 2 : 0;   // 2: the straight-line SpMV per line order
             a.opt = s.ghost ? 0 : c->tune.band_opt;   // variants exist for the one-rank instantiation
-            a.j3 = std::min(c->tune.band_j3, BAND_J3);
-            HIPCHK(c, launch_band_step(a, s.band_grid(j, a.opt, a.j3), s.A->sell.uniform_w, c->stream));
-        } else if (s.sweep) {
-            // update pass of step j + the table SpMV of p_{j+1} (none after the cycle's last step)
-            const bool sp = j + 1 < m;
-            Prof pf(c, "line_sweep", j, n8 * (j + 4) + (sp ? 2 * n8 : 0.0));   // V_j, p, w; v_j, p_{j+1} (+ D, y)
-            LineSweepK a;
-            a.V = s.V;
-            a.ld = s.ld;
-            a.j = j;
-            a.m = m;
-            a.p_in = s.p_of(j);
-            a.p_out = s.pbuf[(j + 1) & 1];
-            a.w = w_cur;
-            a.cf = s.cf;
-            a.st = ds;
-            a.x = s.x;
-            a.H = s.H;
-            a.S = s.S;
-            a.lsv = s.A->d_lsv;
-            a.y = sp ? s.tmp : nullptr;
-            a.n = (int)n;
-            a.L = (int)s.A->band_L;
-            a.H_parts = band_parts(s.A->band_L);
-            HIPCHK(c, launch_line_sweep(a, s.sweep_R, c->stream));
+            HIPCHK(c, launch_band_step(a, s.band_grid(j, a.opt), s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
-            HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, c->tune.upd_grid > 0 ? c->tune.upd_grid : s.G, ds,
-                                       s.x, s.H, s.S, m, fused ? 0 : 1, c->tune.upd_xb, c->stream));
+            HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1, c->stream));
         }
         // throttle: an event every EV_EVERY steps (each record costs the stream a few us); the
         // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
@@ -1508,21 +1476,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     const size_t nghost = (s.band && A->band_ghost)
                               ? (size_t)2 * (m + 2) * A->band_L + 4 * (size_t)BAND_GHOST_VECS * A->band_L : 0;
     const size_t nedge = s.band ? (size_t)s.ld + nghost : 0;
-    // line path: the update pass fused with the next table SpMV (k_line_sweep; one rank, the
-    // line-Jacobi dots kernel, canonical line-separable rows, restart <= 20); p apart from V
-    if (dc && !c->dist && c->tune.line_sweep > 0 && M && M->kind == VTK_PREC_LINE && M->line.seg >= 1 &&
-        M->line.seg <= 32 && A->d_lsv && A->band_L > 0 && A->lsv_canon && c->tune.band_lsv && c->tune.sell_canon &&
-        A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk && A->sell.n_wide == 0 && m <= 20) {
-        const int H = band_parts(A->band_L);
-        const int64_t X = n / A->band_L;
-        if (H >= 1 && X >= 3 && n % A->band_L == 0) {
-            s.sweep = true;
-            s.sweep_R = (int)std::max<int64_t>(1, std::min<int64_t>(c->tune.line_sweep / H, X / 2));
-        }
-    }
-    const size_t npb = s.sweep ? 2 * (size_t)s.ld : 0;
-    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge +
-                      npb + 16;
+    const size_t nd = (size_t)(m + 1) * s.ld + 3 * (size_t)s.ld + (size_t)m * (m + 1) + (m + 1) + 2 * m + 64 + ndc + nedge + 16;
     if (c->ws_bytes < nd * sizeof(double)) {
         if (c->ws) (void)hipFree(c->ws);
         c->ws = nullptr;
@@ -1555,11 +1509,6 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             s.grecv = s.gsend + 2 * (size_t)BAND_GHOST_VECS * A->band_L;
         }
         wp += nedge;
-    }
-    if (s.sweep) {
-        s.pbuf[0] = wp;
-        s.pbuf[1] = wp + s.ld;
-        wp += npb;
     }
     HIPCHK(c, hipMemsetAsync(s.H, 0, (size_t)m * (m + 1) * sizeof(double), c->stream));
     HIPCHK(c, hipMemsetAsync(s.giv, 0, (size_t)2 * m * sizeof(double), c->stream));
@@ -1613,7 +1562,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             dd.p1 = prz;
             int g = 0;
             HIPCHK(c, launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
-                                     c->tune.g4_ring, c->tune.g4_pd, c->tune.g4_xcd, c->tune.g4_gr, &dd, &g, nullptr,
+                                     c->tune.g4_ring, c->tune.g4_gr, &dd, &g, nullptr,
                                      0, c->stream));
             TRY(pad_partials(c, prr, prz, g));
             rr = reduce(c, prr, g, rc2);
@@ -1748,7 +1697,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         // x += y @ V[:col+1] (:799-814), r = b - A x, rnorm (:816-817)
         const size_t xup_idx = c->prof_pending.size();
         { Prof pf(c, "xupdate", -1, 0.0);   // bytes set once the stop column is known
-          HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->tune.upd_xb, c->stream)); }
+          HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream)); }
         TRY(residual());
         HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1760,10 +1709,9 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
                 // the x update ran in update pass xup_tag: account it as the "xupdate" class and
                 // drop the host-enqueued k_xupdate (it returned at entry)
                 const int cu = prof_class(c, "dc_update"), cb = prof_class(c, "band_step"), cx = prof_class(c, "xupdate");
-                const int cw = prof_class(c, "line_sweep");
                 for (size_t i = 0; i < xup_idx && i < c->prof_pending.size(); ++i) {
                     auto &p = c->prof_pending[i];
-                    if ((p.cls == cu || p.cls == cb || p.cls == cw) && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
+                    if ((p.cls == cu || p.cls == cb) && p.col == hs->xup_tag) { p.cls = cx; p.col = -1; p.bytes = xb; }
                 }
                 if (xup_idx < c->prof_pending.size()) c->prof_pending[xup_idx].col = BIG_COL;
             }

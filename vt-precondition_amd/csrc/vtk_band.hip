@@ -38,35 +38,19 @@ namespace vtk {
 // geometry: half lines (LP <= BAND_LP = 400 rows, 7 waves, ~79 KB LDS, two workgroups per CU).
 // Quarter lines with the staged basis double-buffered and every step's next line prefetched
 // (4 waves, 2-4 workgroups per CU by LDS) measured 2-10 % slower per step (round 5).
-#ifndef VTK_BAND_DOTS_UNROLL
-#define VTK_BAND_DOTS_UNROLL 2   // the dots' 64-row passes issued together (LDS latency once per group)
-#endif
-#ifndef VTK_BAND_REREAD
-#define VTK_BAND_REREAD 0   // 1: the dots re-read the line's basis rows from L2 (no LDS staging)
-#endif
-#ifndef VTK_BAND_XUP_INLINE
-#define VTK_BAND_XUP_INLINE 4   // > 0: the cycle's x update inlined into k_band_step, basis loads in batches of
-                                // this many (0: the out-of-line call; C3 xupdate 648-653 -> 641-643 us)
-#endif
-#ifndef VTK_BAND_PF
-#define VTK_BAND_PF (VTK_BAND_REREAD ? 18 : 12)   // j <= this: next line's update operands prefetched across SpMV + dots
-                                                 // (round 3: 10: 567-570 us; 8: 570; 12: 567; 18: 624, spills;
-                                                 // with the fused multiply-adds j <= 12 fits 124 VGPRs)
-#endif
-#ifndef VTK_BAND_GHT
-#define VTK_BAND_GHT 1   // one rank (no ghost lines): the instantiation without the ghost paths
-                         // (band step 563-569 vs 571-575 us, process A/B 3 reps)
-#endif
-#ifndef VTK_BAND_VBUF_FIXED
-#define VTK_BAND_VBUF_FIXED 0   // 1: LDS sized for j = 18 in every instantiation
-#endif
+#define VTK_BAND_DOTS_UNROLL 2   // (a #pragma unroll literal) the dots' 64-row passes issued together
+constexpr int BAND_XUP_XB = 4;     // the cycle's x update inlined into k_band_step, basis loads in batches of
+                                   // this many (C3 x update 648-653 -> 641-643 us)
+constexpr int BAND_PF = 12;        // j <= this: next line's update operands prefetched across SpMV + dots
+                                   // (round 3: 10: 567-570 us; 8: 570; 12: 567; 18: 624, spills; with
+                                   // the fused multiply-adds j <= 12 fits 124 VGPRs)
 
 // VMODE 1 (LSV): the matrix values from the line-separable tables (vtk_csr::d_lsv: the diagonal
 // per row, x +- 1 couplings per position v -- held in registers for the lane's v --, v +- 1
 // couplings per line) instead of the SELL copy's 5 values per row; VMODE 2 (also canonical
 // rows, vtk_csr::lsv_canon): the entries' kinds and order from canon_order instead of the SELL
 // codes and dictionary.  The same values in the same order either way
-// OPT bit 0 (SPF): with the next-line prefetch (J <= VTK_BAND_PF) and canonical rows, the SpMV
+// OPT bit 0 (SPF): with the next-line prefetch (J <= BAND_PF) and canonical rows, the SpMV
 // operands of a line (D, m, the line's v couplings) travel in the same prefetch as the update
 // operands, one line ahead.  Loaded at the head of their own iteration they made the wait for the
 // prefetched update operands a wait for everything (s_waitcnt vmcnt(0): the loads sit in
@@ -86,18 +70,15 @@ template <int WU, int J, int VMODE = 0, bool GH = true, int OPT = 0>
 __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe<OPT>()))) void k_band_step(BandK a) {
     constexpr int BAND_RS = BAND_T;
     constexpr int BAND_W = BAND_T / 64, BAND_IT = (J + 2 + BAND_W - 1) / BAND_W;   // dot items per wave
-    __shared__ double vbuf[VTK_BAND_REREAD ? 1 : (VTK_BAND_VBUF_FIXED ? BAND_JV : J + 1) * BAND_LP];
+    __shared__ double vbuf[(J + 1) * BAND_LP];
     __shared__ double ring[4 * BAND_RS];
     __shared__ double wbuf[BAND_LP];
     __shared__ double red[DC_NQ];
     __shared__ double cs[BAND_JV], ce[BAND_JV], cp[BAND_JV];
     constexpr int j = J;
-    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
-        if constexpr (VTK_BAND_XUP_INLINE > 0)
-            dc_xupdate_body<VTK_BAND_XUP_INLINE, true>(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf,
-                                                     a.x, a.H, a.S, a.m, a.w_prev);
-        else
-            dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, a.w_prev);
+    if (__builtin_nontemporal_load(&a.st->xup_tag) == j) {   // the cycle's x update
+        dc_xupdate_body<BAND_XUP_XB, true>(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x,
+                                           a.H, a.S, a.m, a.w_prev);
         return;
     }
     if (stopped(&a.st->stop_col, j)) return;
@@ -138,10 +119,10 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
         kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
         return it == 0 ? xhm : (it == nl + 1 ? xhp : xa - 1 + it);
     };
-    // software pipeline (J <= VTK_BAND_PF, as the registers allow): the next line's update
+    // software pipeline (J <= BAND_PF, as the registers allow): the next line's update
     // operands are loaded during this line's SpMV and dots.  (A partial prefetch of 4 basis rows
     // for larger J measured slower: 1234 vs 1254 it/s, spills)
-    constexpr bool PF = J <= VTK_BAND_PF;
+    constexpr bool PF = J <= BAND_PF;
     constexpr bool SPF = PF && CANON && (OPT & 1);
     // update operands of iteration it's line on the lane's row: V_k (k < j), w_{j-1} (j = 0: v_0)
     // and w_j
@@ -195,7 +176,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             const double *pv = a.V + row;
 #pragma unroll
             for (int k = 0; k < J; ++k) {
-                o.v[k] = upd ? (VTK_BAND_REREAD ? *pv : __builtin_nontemporal_load(pv)) : 0.0;
+                o.v[k] = upd ? __builtin_nontemporal_load(pv) : 0.0;
                 pv += a.ld;
             }
         }
@@ -229,15 +210,14 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
         vreg[J] = vj;
         if (kind == 0 && own) {
             if (j >= 1) {
-                if constexpr (VTK_BAND_REREAD) a.V[(size_t)j * a.ld + row] = vj;
-                else __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+                __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
             }
             if (j == a.m - 2) __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
         }
         return pn;
     };
     auto stage = [&](double *vb) {
-        if (!VTK_BAND_REREAD && own) {
+        if (own) {
 #pragma unroll
             for (int k = 0; k <= J; ++k) vb[k * BAND_LP + tid - 8] = vreg[k];
         }
@@ -406,8 +386,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             for (int u = 0; u < BAND_IT; ++u) {
                 const int itm = wv + BAND_W * u;
                 if (itm <= j) {
-                    const double *vk = VTK_BAND_REREAD ? a.V + (size_t)itm * a.ld + (int64_t)x * L + v0
-                                                       : vbuf + itm * BAND_LP;
+                    const double *vk = vbuf + itm * BAND_LP;
 #pragma unroll VTK_BAND_DOTS_UNROLL
                     for (int t = lane; t < LP; t += 64) {
                         const double vv = vk[t];
@@ -459,8 +438,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
 template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipStream_t s) {
     const dim3 g(grid), blk(BAND_T);
     if constexpr (J <= BAND_J3) {
-        if (J > a.j3) {}
-        else if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 3>), g, blk, 0, s, a); return; }
+        if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 3>), g, blk, 0, s, a); return; }
         if ((a.opt & 3) == 2) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 2>), g, blk, 0, s, a); return; }
     }
     if (a.opt & 1) hipLaunchKernelGGL((k_band_step<5, J, 2, false, 1>), g, blk, 0, s, a);
@@ -475,7 +453,7 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     switch (a.j) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
-        if (a.lsv && a.canon && VTK_BAND_GHT && !a.ghost) launch_band_one_rank<J_>(a, grid, s); \
+        if (a.lsv && a.canon && !a.ghost) launch_band_one_rank<J_>(a, grid, s); \
         else if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, 2>), dim3(grid), dim3(BAND_T), 0, s, a); \
         else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, 1>), dim3(grid), dim3(BAND_T), 0, s, a); \
         else hipLaunchKernelGGL((k_band_step<5, J_>), dim3(grid), dim3(BAND_T), 0, s, a); \
@@ -849,7 +827,7 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
 // [g0 - S3, g0 + 256 + S3) (S3 = Nvx Nvy, the y-line), so the vy, vx and y couplings read LDS, and
 // the window slides by one group per step.  Every global operand of a group -- the window's next
 // 256 rows, the x -+ 1 plane rows (S4 away: contiguous 256-row blocks), the y-wrap row, m and D --
-// is loaded PD groups ahead into a register queue, all loads unconditional (clamped rows, the
+// is loaded one group ahead into registers, all loads unconditional (clamped rows, the
 // halo chosen by address): no exec-masked load, so the wait for a group's operands does not wait
 // for the groups behind it.  Coordinates advance by 256 in the mixed radix (no division per row),
 // ring slots by 256 modulo RL.  Terms summed in the stored order (as k_sell's grid rows), the BJ
@@ -857,29 +835,21 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
 // RL: ring length (>= 2 S3 + 512): 4608 (36 KB, four workgroups per CU) when the y-line allows
 // (C4: S3 = 2000), else 8192 (64 KB); the tables TX | TY | TVX | TVY (<= G4TAB doubles) in LDS
 // too: three workgroups per CU at C4.
-// DC: the DCGS2 step j fused in (x = p_j = V[j]): s = V_j^T p, z = V_j^T w, |p|^2, p.w, |w|^2 per
-// workgroup in launch_dc_dots' partial layout.  Each group's p and w are staged in LDS (two
-// buffers) and wave wv reads the group's rows of V[k], k = wv, wv + 4, ... (the split of
-// dc_rows); the w write stays (the update pass reads it).
-// MODE (G4Dots::mode): 0 w = M^-1 A x; 1 DC (the dots above); 2 DCGS2 step 0 (j = 0: |p|^2,
-// p.w, |w|^2, each lane over its own rows); 3 the cycle-start residual r = b - A x, w = M^-1 r,
-// |r|^2, |w|^2 (partials p0, p1) -- k_sell<EPI_RESID_PREC>'s operations.  Modes 1-3: one partial
-// per workgroup, lanes -> waves -> workgroup in a fixed order.
-template <typename VT, bool HALO, int RL, int PD, int MODE, int GR>
-__global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 && RL <= 5120 && MODE != 1 ? 6 : 1))) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
+// MODE (G4Dots::mode): 0 w = M^-1 A x; 2 DCGS2 step 0 (j = 0: |p|^2, p.w, |w|^2, each lane over
+// its own rows); 3 the cycle-start residual r = b - A x, w = M^-1 r, |r|^2, |w|^2 (partials p0,
+// p1) -- k_sell<EPI_RESID_PREC>'s operations.  Modes 2-3: one partial per workgroup, lanes ->
+// waves -> workgroup in a fixed order.  (Round 5 removed mode 1, the later steps' dots fused in:
+// 215.6 vs 201.5 ms per C4 solve)
+template <typename VT, bool HALO, int RL, int MODE, int GR>
+__global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 && RL <= 5120 ? 6 : 1))) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
                                                 const double *__restrict__ mtri, double *__restrict__ w, int n,
                                                 int ngroups_per_wg, int g_lo, int g_hi, G4Dots dd, const int *stop_col,
                                                 int col) {
-    constexpr bool DC = MODE == 1, RES = MODE == 3;
+    constexpr bool RES = MODE == 3;
     __shared__ double ring[RL];
     __shared__ double tb[G4TAB];
     __shared__ double red3[3][MODE >= 2 ? GR / 64 : 1];
-    constexpr int KPW = DC_MAXJ / (GR / 64);
-    __shared__ double pw[DC ? 2 : 1][DC ? 2 * GR : 1];
-    double ds_[KPW], dz_[KPW], daa = 0.0, dab = 0.0, dag = 0.0;
     double e0 = 0.0, e1 = 0.0, e2 = 0.0;   // MODE 2 / 3: the lane's sums over its rows
-#pragma unroll
-    for (int u = 0; u < KPW; ++u) ds_[u] = dz_[u] = 0.0;
     if (stopped(stop_col, col)) return;
     const int tid = threadIdx.x, lane = tid & 63, ii = lane & 7;
     const int Nvy = g.Nvy, Nvx = g.Nvx, Ny = g.Ny;
@@ -890,8 +860,7 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
         if (MODE >= 1 && threadIdx.x < DC_NQ) {
             const int q = threadIdx.x;
             if (MODE == 3) { if (q == 0) dd.p0[pslot] = 0.0; if (q == 1) dd.p1[pslot] = 0.0; }
-            else if (MODE == 2 ? q >= 2 * DC_MAXJ : (q < dd.j || (q >= DC_MAXJ && q < DC_MAXJ + dd.j) || q >= 2 * DC_MAXJ))
-                dd.part[(size_t)q * GMAX + pslot] = 0.0;
+            else if (q >= 2 * DC_MAXJ) dd.part[(size_t)q * GMAX + pslot] = 0.0;
         }
         return;
     }
@@ -961,9 +930,8 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
         o.c = lead;
         adv(lead);
     };
-    Ld qu[PD];
-#pragma unroll
-    for (int k = 0; k < PD; ++k) load(gb + k, qu[k]);
+    Ld nx;
+    load(gb, nx);
     int sb = (gb * GR + tid) % RL;   // ring slot of the lane's row
     auto slot = [&](int off) {
         int t = sb + off;
@@ -973,10 +941,8 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
     };
     __syncthreads();
     for (int gi = gb; gi < ge; ++gi) {
-        const Ld cu = qu[0];
-#pragma unroll
-        for (int k = 0; k + 1 < PD; ++k) qu[k] = qu[k + 1];
-        load(gi + PD, qu[PD - 1]);
+        const Ld cu = nx;
+        load(gi + 1, nx);
         const int r = gi * GR + tid;
         const bool act = r < n;
         const int rc = act ? r : n - 1;
@@ -1032,63 +998,11 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
                 e2 += z * z;
             }
         }
-        const int buf = gi & 1;
-        if constexpr (DC) {
-            pw[buf][tid] = act ? x0 : 0.0;
-            pw[buf][GR + tid] = act ? z : 0.0;
-        }
         // slide the window: the rows of group gi + 1's upper edge (their slots held rows the
         // remaining groups no longer read; the ring is > 2 S3 + 512 long)
         if (r + GR + S3 < n) ring[slot(GR + S3)] = cu.xn;
         sb = slot(GR);
         __syncthreads();
-        if constexpr (DC) {
-            // the group's dots (the other buffer is written next; this one again only after the
-            // next barrier, which every wave reaches after these reads)
-            const int wv = tid >> 6;
-            const double *pt = pw[buf], *wt = pw[buf] + GR;
-#pragma unroll
-            for (int u = 0; u < KPW; ++u) {
-                const int k = wv + u * (GR / 64);
-                if (k < dd.j) {
-                    const double *vk = dd.V + (size_t)k * dd.ld;
-#pragma unroll
-                    for (int h = 0; h < GR / 64; ++h) {
-                        const int i = lane + 64 * h;
-                        const double v = __builtin_nontemporal_load(vk + min(gi * GR + i, n - 1));
-                        ds_[u] += v * pt[i];
-                        dz_[u] += v * wt[i];
-                    }
-                }
-            }
-            if (wv == 0) {
-#pragma unroll
-                for (int h = 0; h < GR / 64; ++h) {
-                    const int i = lane + 64 * h;
-                    daa += pt[i] * pt[i];
-                    dab += pt[i] * wt[i];
-                    dag += wt[i] * wt[i];
-                }
-            }
-        }
-    }
-    if constexpr (DC) {
-        // per-workgroup partials (dc_write's layout); the ring is free now
-        const int wv = tid >> 6;
-        double *red = ring;
-#pragma unroll
-        for (int u = 0; u < KPW; ++u) {
-            const int k = wv + u * (GR / 64);
-            const double ts = wave_sum(ds_[u]), tz = wave_sum(dz_[u]);
-            if (lane == 0 && k < dd.j) { red[k] = ts; red[DC_MAXJ + k] = tz; }
-        }
-        const double t0 = wave_sum(daa), t1 = wave_sum(dab), t2 = wave_sum(dag);
-        if (wv == 0 && lane == 0) { red[2 * DC_MAXJ] = t0; red[2 * DC_MAXJ + 1] = t1; red[2 * DC_MAXJ + 2] = t2; }
-        __syncthreads();
-        for (int q = tid; q < DC_NQ; q += GR) {
-            const bool used = q < dd.j || (q >= DC_MAXJ && q < DC_MAXJ + dd.j) || q >= 2 * DC_MAXJ;
-            if (used) dd.part[(size_t)q * GMAX + pslot] = red[q];
-        }
     }
     if constexpr (MODE >= 2) {
         const int wid = tid >> 6;
@@ -1111,22 +1025,18 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
 }
 
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
-                          int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out,
-                          const int *stop_col, int col, hipStream_t s, int g_lo, int g_hi, int per_in) {
-    // gr: rows per group = lanes per workgroup (256, or 512 without the fused dots of mode 1)
+                          int fp32, int wgs, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
+                          int col, hipStream_t s, int g_lo, int g_hi, int per_in) {
+    // gr: rows per group = lanes per workgroup (256 or 512)
     const int mode = dots ? dots->mode : 0;
-    const int G = g4_ring_group(gr, mode);
+    const int G = g4_ring_group(gr);
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy, S4 = S3 * g.Ny;
-    if (!g.tab || !g.D || !g4_ring_fits(g, n, gr, mode) || S4 <= 0 || n % S4 || (halo == nullptr) != (g.lblk < 0))
+    if (!g.tab || !g.D || !g4_ring_fits(g, n, gr) || S4 <= 0 || n % S4 || (halo == nullptr) != (g.lblk < 0))
         return hipErrorInvalidValue;
     // the ring: the window 2 S3 + G plus the next group's rows
     const bool small = 2 * S3 + 2 * G <= (G == 256 ? 4608 : 5120);
     const int64_t ng = (n + G - 1) / G;
     int64_t per = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
-    // xcd > 0: ranges of S4 / xcd rows, so that the ranges reading a range's rows as their x -+ 1
-    // planes are xcd workgroups away -- on the same XCD (workgroups are dealt round-robin over the
-    // eight XCDs) when xcd is a multiple of 8: those reads hit that XCD's L2
-    if (xcd > 0) per = std::max<int64_t>(1, (S4 + G / 2 * xcd) / (G * (int64_t)xcd));
     // the fused reductions write one partial per workgroup: at most GMAX workgroups
     if (mode) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
     // a group range [g_lo, g_hi) of the launch (the interior / boundary planes of a rank's slab
@@ -1137,30 +1047,25 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
     const int64_t span = std::max<int64_t>(1, g_hi - g_lo);
     const dim3 grid((unsigned)((span + per - 1) / per)), blk(G);
     if (mode && (dots->part_off < 0 || dots->part_off + (int64_t)grid.x > GMAX)) return hipErrorInvalidValue;
-    if (mode < 0 || mode > 3 || (mode == 1 && (dots->j < 0 || dots->j > DC_MAXJ || !dots->V || !dots->part)) ||
-        (mode == 2 && !dots->part) || (mode == 3 && (!dots->b || !dots->p0 || !dots->p1)))
+    if (mode == 1 || mode < 0 || mode > 3 || (mode == 2 && !dots->part) ||
+        (mode == 3 && (!dots->b || !dots->p0 || !dots->p1)))
         return hipErrorInvalidValue;
     if (grid_out) *grid_out = (int)grid.x;
     const G4Dots dd = dots ? *dots : G4Dots{};
-#define VTK_G4R(VT_, H_, RL_, PD_, DC_, GR_) \
-    hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, PD_, DC_, GR_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, \
-                       g_lo, g_hi, dd, stop_col, col)
+#define VTK_G4R(VT_, H_, RL_, M_, GR_) \
+    hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, M_, GR_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, g_lo, \
+                       g_hi, dd, stop_col, col)
 #define VTK_G4R_M(VT_, H_, RL_, GR_) \
     do { \
-        if (mode == 1) VTK_G4R(VT_, H_, RL_, 1, 1, GR_); \
-        else if (mode == 2) VTK_G4R(VT_, H_, RL_, 1, 2, GR_); \
-        else if (mode == 3) VTK_G4R(VT_, H_, RL_, 1, 3, GR_); \
-        else VTK_G4R(VT_, H_, RL_, 1, 0, GR_); \
+        if (mode == 2) VTK_G4R(VT_, H_, RL_, 2, GR_); \
+        else if (mode == 3) VTK_G4R(VT_, H_, RL_, 3, GR_); \
+        else VTK_G4R(VT_, H_, RL_, 0, GR_); \
     } while (0)
 #define VTK_G4R_PD(VT_, H_) \
     do { \
         if (G == 512) { if (small) VTK_G4R_M(VT_, H_, 5120, 512); else VTK_G4R_M(VT_, H_, 8192, 512); } \
-        else if (!small) VTK_G4R_M(VT_, H_, 8192, 256); \
-        else if (mode) VTK_G4R_M(VT_, H_, 4608, 256); \
-        else if (pd <= 1) VTK_G4R(VT_, H_, 4608, 1, 0, 256); \
-        else if (pd == 2) VTK_G4R(VT_, H_, 4608, 2, 0, 256); \
-        else if (pd == 3) VTK_G4R(VT_, H_, 4608, 3, 0, 256); \
-        else VTK_G4R(VT_, H_, 4608, 4, 0, 256); \
+        else if (small) VTK_G4R_M(VT_, H_, 4608, 256); \
+        else VTK_G4R_M(VT_, H_, 8192, 256); \
     } while (0)
     if (fp32) {
         if (halo) VTK_G4R_PD(float, true);
@@ -1172,148 +1077,6 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
 #undef VTK_G4R_PD
 #undef VTK_G4R_M
 #undef VTK_G4R
-    return hipGetLastError();
-}
-
-// the canonical table SpMV of line xl (one rank) from a ring of x lines: slots sm (x-1), sx (x),
-// sp (x+1), lane tid <-> position v; the same products in the same order as k_lsv_spmv<CANON>
-__device__ __forceinline__ double ring_line_spmv(const double *ring, int sm, int sx, int sp, int tid, int v, int L,
-                                                 int X, int n, int xl, double tx0, double tx1, double drow,
-                                                 const double *__restrict__ lsv) {
-    const double tv0 = lsv[n + 2 * L + xl], tv1 = lsv[n + 2 * L + X + xl];
-    int64_t cxm, cxp;
-    const int ord = __builtin_amdgcn_readfirstlane(canon_order_xv(xl, 0, n, L, X, -1, cxm, cxp));
-    constexpr int P_MID = 0 | 1 << 3 | 2 << 6 | 3 << 9 | 4 << 12;
-    constexpr int P_FIRST = 1 | 2 << 3 | 3 << 6 | 4 << 9 | 0 << 12;
-    const double t0 = tx0 * ring[sm + tid];
-    const double t4 = tx1 * ring[sp + tid];
-    const double t2 = drow * ring[sx + tid];
-    const double t1 = tv0 * ring[sx + tid - (tid > 0 ? 1 : 0)];
-    const double t3 = tv1 * ring[sx + tid + (tid < BAND_T - 1 ? 1 : 0)];
-    const bool h1 = v > 0, h3 = v < L - 1;
-    double sa = 0.0;
-    if (ord == P_MID) {
-        sa = sa + t0;
-        sa = h1 ? sa + t1 : sa;
-        sa = sa + t2;
-        sa = h3 ? sa + t3 : sa;
-        sa = sa + t4;
-    } else if (ord == P_FIRST) {   // line 0: x-1 wraps to line X-1, last
-        sa = h1 ? sa + t1 : sa;
-        sa = sa + t2;
-        sa = h3 ? sa + t3 : sa;
-        sa = sa + t4;
-        sa = sa + t0;
-    } else {                        // line X-1: x+1 wraps to line 0, first
-        sa = sa + t4;
-        sa = sa + t0;
-        sa = h1 ? sa + t1 : sa;
-        sa = sa + t2;
-        sa = h3 ? sa + t3 : sa;
-    }
-    return sa;
-}
-
-// Line path: k_dc_update's pass of step j and the table SpMV of p_{j+1} in one walk over the
-// x-lines: the workgroup of (range, part) updates line y (its rows and one v-halo
-// row each side; the x-halo lines before and after the range recomputed, not stored), puts
-// p_{j+1}(y) into an LDS ring of 4 lines, and forms y = A p_{j+1} on line y - 1 from the ring.
-// p_{j+1} is not re-read for the SpMV; one launch instead of two.  The next line's operands are
-// loaded one line ahead.  Same operations as k_dc_update and k_lsv_spmv<CANON>: bit-identical.
-template <int J>
-__global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(4))) void k_line_sweep(LineSweepK a) {
-    constexpr int j = J;
-    __shared__ double ring[4 * BAND_T];
-    __shared__ double cs[BAND_JV + 1], ce[BAND_JV + 1];
-    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&a.st->xup_tag) == j) {
-        dc_xupdate(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x, a.H, a.S, a.m, nullptr,
-                   a.p_in);
-        return;
-    }
-    if (stopped(&a.st->stop_col, j)) return;
-    const int tid = threadIdx.x, n = a.n, L = a.L, X = n / L, LP = L / a.H_parts;
-    const int b = blockIdx.x, R = (int)gridDim.x / a.H_parts, rb = b / a.H_parts, h = b % a.H_parts, v0 = h * LP;
-    const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R), nl = xb - xa;
-    const int v = v0 - 8 + tid;
-    const bool inl = v >= 0 && v < L && tid < LP + 16;   // the part's rows and its v-halo rows
-    const bool own = tid >= 8 && tid < 8 + LP;
-    const bool spmv = a.y != nullptr;
-    for (int k = tid; k <= j; k += BAND_T) {
-        if (k < j) cs[k] = a.cf->s[k];
-        ce[k] = a.cf->e[k];
-    }
-    const double rinv = a.cf->rinv, q = a.cf->q;
-    const double tx0 = own ? a.lsv[n + v] : 0.0, tx1 = own ? a.lsv[n + L + v] : 0.0;
-    __syncthreads();
-    const double ej = ce[j];
-    auto line_of = [&](int it) { return it == 0 ? (xa == 0 ? X - 1 : xa - 1) : (it == nl + 1 ? (xb == X ? 0 : xb) : xa - 1 + it); };
-    struct Ld {
-        double v[J > 0 ? J : 1];
-        double p, w, drow;
-    };
-    // every lane loads (rows outside the part clamped to v0, their values unused): no exec-mask
-    // blocks around the loads, so the wait for this line's operands need not wait for the next's
-    const int vc = inl ? v : v0;
-    auto load = [&](int it, Ld &o) {
-        const int64_t row = (int64_t)line_of(it) * L + vc;
-        o.p = __builtin_nontemporal_load(a.p_in + row);
-        o.w = __builtin_nontemporal_load(a.w + row);
-        const double *pv = a.V + row;
-#pragma unroll
-        for (int k = 0; k < J; ++k) {
-            o.v[k] = __builtin_nontemporal_load(pv);
-            pv += a.ld;
-        }
-        const int xs = it >= 2 ? xa + it - 2 : xa;
-        o.drow = __builtin_nontemporal_load(a.lsv + (int64_t)xs * L + vc);
-    };
-    Ld nx;
-    load(0, nx);
-    for (int it = 0; it <= nl + 1; ++it) {
-        const Ld cu = nx;
-        double av = cu.p, t = cu.w;
-#pragma unroll
-        for (int k = 0; k < J; ++k) {
-            const double sk = cs[k], ek = ce[k];
-            av = av - sk * cu.v[k];
-            t = t - ek * cu.v[k];
-        }
-        double vj = cu.p;
-        if (j >= 1) vj = av * rinv;
-        t = t - ej * vj;
-        const double pn = t * q;
-        if (it >= 1 && it <= nl && own) {   // an owned line: store v_j and p_{j+1}
-            const int64_t row = (int64_t)(xa - 1 + it) * L + v;
-            if (j >= 1) __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
-            __builtin_nontemporal_store(pn, a.p_out + row);
-        }
-        ring[(it & 3) * BAND_T + tid] = inl ? pn : 0.0;
-        if (it <= nl) load(it + 1, nx);
-        __syncthreads();
-        if (spmv && it >= 2) {
-            const int xl = xa + it - 2;
-            const double s = ring_line_spmv(ring, ((it - 2) & 3) * BAND_T, ((it - 1) & 3) * BAND_T, (it & 3) * BAND_T, tid,
-                                            v, L, X, n, xl, tx0, tx1, cu.drow, a.lsv);
-            if (own) __builtin_nontemporal_store(s, a.y + (int64_t)xl * L + v);
-        }
-    }
-}
-
-hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s) {
-    const int H = a.H_parts;
-    if (H < 1 || a.L % H != 0 || a.L / H > BAND_LP || (a.L / H) % 8 != 0 || a.n % a.L != 0 || a.n / a.L < 3 ||
-        ranges < 1 || ranges > a.n / a.L / 2 || a.j + 1 > BAND_JV + 1)
-        return hipErrorInvalidValue;
-    const dim3 g((unsigned)(ranges * H)), blk(BAND_T);
-    switch (a.j) {
-#define VTK_SWEEP_J(J_) \
-    case J_: hipLaunchKernelGGL((k_line_sweep<J_>), g, blk, 0, s, a); break;
-        VTK_SWEEP_J(0) VTK_SWEEP_J(1) VTK_SWEEP_J(2) VTK_SWEEP_J(3) VTK_SWEEP_J(4) VTK_SWEEP_J(5) VTK_SWEEP_J(6)
-        VTK_SWEEP_J(7) VTK_SWEEP_J(8) VTK_SWEEP_J(9) VTK_SWEEP_J(10) VTK_SWEEP_J(11) VTK_SWEEP_J(12) VTK_SWEEP_J(13)
-        VTK_SWEEP_J(14) VTK_SWEEP_J(15) VTK_SWEEP_J(16) VTK_SWEEP_J(17) VTK_SWEEP_J(18) VTK_SWEEP_J(19)
-#undef VTK_SWEEP_J
-        default: return hipErrorInvalidValue;
-    }
     return hipGetLastError();
 }
 

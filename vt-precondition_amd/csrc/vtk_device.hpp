@@ -211,26 +211,20 @@ __device__ __forceinline__ T ldnt(const T *p) { return __builtin_nontemporal_loa
 __device__ __forceinline__ d2v ldnt2(const double *p) {
     return __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
 }
-// non-temporal vector stores (A/B: streamed-out results that are re-read only by a later
-// kernel gain; VTK_NT_MISC bits: 1 scale0 / x update (neutral, off), 2 SpMV epilogues (plain
-// SpMV 243 -> 223 us), 4 line apply (line solve +0.8 %))
-#ifndef VTK_NT_MISC
-#define VTK_NT_MISC 6
-#endif
-// non-temporal loads of operands read once per kernel (VTK_NT_LOADS bits: 1 fused BJ m,
-// 4 dots p/w, 8 line apply r/m; the update pass chooses per path, k_dc_update<NTPW>).
-// A/B: 1 = +2.5 % (C3 BJ path), 4|8 = +1 % (line path)
-#ifndef VTK_NT_LOADS
-#define VTK_NT_LOADS 13
-#endif
+// cache policy per operand class ("Cache policy"): non-temporal vector stores of
+// streamed-out results re-read only by a later kernel (NT_STORES bits: 1 scale0 / x update --
+// neutral, off; 2 SpMV epilogues, plain SpMV 243 -> 223 us; 4 line apply, line solve +0.8 %) and
+// non-temporal loads of operands read once per kernel (NT_LOADS bits: 1 fused BJ m, +2.5 % on
+// the C3 BJ path; 4 dots p/w and 8 line apply r/m, +1 % on the line path)
+constexpr int NT_STORES = 6, NT_LOADS = 13;
 template <int BIT>
 __device__ __forceinline__ double ld_nt(const double *p) {
-    if constexpr ((VTK_NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
+    if constexpr ((NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
     else return *p;
 }
 template <int BIT>
 __device__ __forceinline__ double2 ld_nt2(const double *p) {
-    if constexpr ((VTK_NT_LOADS & BIT) != 0) {
+    if constexpr ((NT_LOADS & BIT) != 0) {
         const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
         return make_double2(v.x, v.y);
     } else {
@@ -239,12 +233,12 @@ __device__ __forceinline__ double2 ld_nt2(const double *p) {
 }
 template <int BIT>
 __device__ __forceinline__ void st_nt(double *p, double v) {
-    if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(v, p);
+    if constexpr ((NT_STORES & BIT) != 0) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 template <int BIT>
 __device__ __forceinline__ void st_nt2(double *p, double x, double y) {
-    if constexpr ((VTK_NT_MISC & BIT) != 0) __builtin_nontemporal_store(d2v{x, y}, reinterpret_cast<d2v *>(p));
+    if constexpr ((NT_STORES & BIT) != 0) __builtin_nontemporal_store(d2v{x, y}, reinterpret_cast<d2v *>(p));
     else *reinterpret_cast<double2 *>(p) = make_double2(x, y);
 }
 
@@ -397,12 +391,7 @@ __device__ inline void hess_solve(const double *__restrict__ H, const double *__
 }
 
 // v_j = (p_j - sum_k s_k v_k) / r  (in place, j >= 1);  p_{j+1} = (w - sum_k e_k v_k - e_j v_j) * q
-#ifndef VTK_UPD_NT
-#define VTK_UPD_NT 2   // non-temporal stores in the update pass: 1 v_j, 2 v_j and p_{j+1} (A/B: 2 = +2.6 % it/s)
-#endif
-#ifndef VTK_XUP_FUSED
-#define VTK_XUP_FUSED 1   // the cycle's x update inside the stopping step's update pass (one basis read less per cycle)
-#endif
+// (the update pass stores v_j and p_{j+1} non-temporal: A/B +2.6 % it/s)
 // The cycle's x update in the update pass of the step whose scalar kernel stopped it (xup_tag):
 // c = stop_col is j-1 (column j-1 finalised in step j: V[0..j-1] all stored) or j (column j
 // committed early: v_j = (p_j - V_j s) / r formed here exactly as the normal pass would store
@@ -511,13 +500,5 @@ static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict_
     }
 }
 
-// the band-step kernels call the x update out of line (their register allocation stays their own);
-// k_dc_update inlines dc_xupdate_body (global, not flat, loads)
-[[maybe_unused]] static __device__ __noinline__ void dc_xupdate(const double *__restrict__ V, int64_t ld, int j, int c, int64_t n,
-                                        const DcCoef *cf, double *__restrict__ x, const double *__restrict__ H,
-                                        const double *__restrict__ S, int m, const double *__restrict__ wprev,
-                                        const double *__restrict__ pj_at = nullptr) {
-    dc_xupdate_body<1>(V, ld, j, c, n, cf, x, H, S, m, wprev, pj_at);
-}
 
 }  // namespace vtk

@@ -140,10 +140,10 @@ inline size_t grid4_tab_len(const Grid4 &g) { return 2 * ((size_t)g.Nvx + g.Nvy 
 // gr >= 512 outside the fused-dots mode 1, else 256).  The solver takes the ring step only for grids
 // that fit (else the SELL grid-row kernels); launch_g4_ring refuses the others
 constexpr int G4TAB = 1024;
-inline int g4_ring_group(int gr, int mode) { return gr >= 512 && mode != 1 ? 512 : 256; }
-inline bool g4_ring_fits(const Grid4 &g, int64_t n, int gr, int mode) {
+inline int g4_ring_group(int gr) { return gr >= 512 ? 512 : 256; }
+inline bool g4_ring_fits(const Grid4 &g, int64_t n, int gr) {
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy;
-    return n > 0 && n <= INT32_MAX / 2 && 2 * S3 + 2 * g4_ring_group(gr, mode) <= 8192 && grid4_tab_len(g) <= (size_t)G4TAB;
+    return n > 0 && n <= INT32_MAX / 2 && 2 * S3 + 2 * g4_ring_group(gr) <= 8192 && grid4_tab_len(g) <= (size_t)G4TAB;
 }
 
 // Tuning switches of a context (vtk_ctx_set_tuning): the defaults are the
@@ -155,43 +155,22 @@ struct Tuning {
     int band_lsv = 1;         // solver launches read the line-separable values (else SELL values)
     int sell_canon = 1;       // ... and canonical rows' columns from the line index (no codes)
     int band_canon = 1;       // the band step reads no codes on canonical rows
-    int band_canon_sl = 1;    // ... with the straight-line SpMV per line order
-    int sell_pad = 1;         // pad nearly uniform SELL widths (<= 2 % more entries)
-    int sell_grid = 0;        // workgroups of the SELL solver launches (0: from the size)
-    int plain_grid = 2048;    // workgroups of the plain SELL SpMV
-    int sell_swz = 1;         // SELL launches walk their groups in XCD-contiguous order: bit 0 the
-                              // plain SpMV (vtk_spmv; C3 PMC 1.40 -> 1.07 GB per launch, time
-                              // neutral), bit 1 the other epilogues (their partials follow the order)
-    int plain_var = 1;        // plain SELL SpMV variant bits (k_sell VAR: 1 = padding gathers branched;
-                              // in-process A/B C3: 243.6 -> 221.3 us, the round-1 kernel's 218-222 us)
     int band_opt = 3;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
                               // C3: SpMV operands prefetched j00 254 -> 217 us, + three workgroups per
-                              // CU for j <= 2: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms)
-    int band_j3 = 2;          // ... bit 1 (three workgroups per CU) for steps j <= band_j3
-    int lsv_spmv_cap = 8192;  // workgroups of the line path's table SpMV
-    int lsv_ring = 2048;      // > 0: that table SpMV with x staged through LDS, ~that many workgroups
-                              // (in-process A/B, C3 line solve: 8.64 -> 8.26 ms; table SpMV 167 -> 105 us)
-    int line_sweep = 0;       // > 0: line path update pass fused with the next table SpMV, ~that many workgroups
-                              // (with the ring SpMV on: 8.11 -> 8.19 ms at 512, slower at 256 / 1024: off)
-    int ev_every = 1;         // host throttle event every this many Arnoldi steps (1..LOOKAHEAD+1)
+                              // CU for j <= BAND_J3: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms)
+    int lsv_ring = 2048;      // > 0: the line path's table SpMV with x staged through LDS, ~that many
+                              // workgroups (in-process A/B, C3 line solve: 8.64 -> 8.26 ms; 167 -> 105 us)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
-    int debug_band = 0;       // band-check trace on stderr
     int comm_solo = 0;        // vtk_comm_init with world 1 builds a one-rank RCCL communicator
-    int auto_band = 1;        // vtk_csr_create detects the line band (drop-in path)
+    int auto_band = 1;        // vtk_csr_create detects the line band and the 4D grid (drop-in path)
     int grid4 = 1;            // solver launches read 4D grid rows from their coordinates (Grid4)
-    int c4_fused = 1;         // with grid4: the DCGS2 dots fused into the 9-wide SELL step
+    int c4_fused = 1;         // with grid4 and no ring: the DCGS2 dots fused into the 9-wide SELL step
     int g4_ring = 2048;       // > 0: the split step's SpMV + BJ of grid rows with x staged through LDS
-                              // (k_g4_ring, ~that many workgroups); takes precedence over c4_fused
-    int g4_pd = 1;            // k_g4_ring: groups of operands loaded ahead (1..4)
-    int g4_xcd = 0;           // k_g4_ring: > 0: ranges of S4 / g4_xcd rows (overrides g4_ring's count)
-    int g4_dc = 0;            // k_g4_ring: the DCGS2 step's dots fused in
-    int g4_dc0 = 1;           // k_g4_ring: step 0's dots (|p|^2, p.w, |w|^2) fused in
-    int g4_res = 1;           // k_g4_ring: the cycle-start residual + BJ (r = b - A x) too
+                              // (k_g4_ring, ~that many workgroups), step 0's dots and the cycle-start
+                              // residual in it too; takes precedence over c4_fused
     int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
-    int upd_grid = 0;         // k_dc_update workgroups (0: the dots grid)
     int cyc_ring = 512;       // > 0: cycle-start residual and DCGS2 step 0 through the x-line ring
-                              // (k_lsv_ring_epi, ~that many workgroups; 2D line-separable, one rank)
-    int upd_xb = 0;           // k_dc_update, k_xupdate: basis rows loaded in batches of 8 (A/B: neutral)
+                              // (k_lsv_ring_epi, ~that many workgroups; 2D line-separable rows)
 };
 }  // namespace vtk
 
@@ -317,10 +296,10 @@ struct SpmvIn {
     int lsv_L = 0, lsv_lblk = -1;
     int lsv_xord = 0;    // across ranks: the halo lines' place in the stored order (vtk_csr::band_xord)
     int lsv_canon = 0;   // ... and every row canonical: k_sell computes the columns (canon_row)
-    int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX; vtk::Tuning)
+    int plain_grid = 0;  // workgroups of the plain SELL SpMV (0: 2 GMAX)
     Grid4 g4{};          // 4D grid rows (solver launches; g4.tab null: not used)
-    int swz = 0;         // XCD-aware SELL group order (vtk::Tuning::sell_swz)
-    int plain_var = 0;   // plain SELL SpMV variant bits (vtk::Tuning::plain_var; k_sell VAR)
+    int swz = 0;         // XCD-aware SELL group order: bit 0 the plain SpMV, bit 1 the other epilogues
+    int plain_var = 0;   // plain SELL SpMV variant bits (k_sell VAR)
 };
 
 LineOp line_plan(int64_t n, int64_t row0, int64_t stride, int64_t seg);
@@ -405,8 +384,7 @@ hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresSt
 // y = triangular solve (H, S) at stop column; x += y @ V
 // (returns at entry when a DCGS2 update pass already did it: st->xup_tag >= 0)
 hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld,
-                          double *x, int64_t n, int m, const GmresState *st, int grid, int xb,
-                          hipStream_t s);
+                          double *x, int64_t n, int m, const GmresState *st, int grid, hipStream_t s);
 // dst = sqrt(reduce(p)) if do_sqrt else reduce(p)   (single workgroup)
 hipError_t launch_finalize(Red p, double *dst, int do_sqrt, hipStream_t s);
 // part = sum x^2 (or x*y)
@@ -447,7 +425,7 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 // c = j the v_j of the pass is formed in registers), reading the basis once
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n,
                             const DcCoef *cf, int grid, const GmresState *st, double *x,
-                            const double *H, const double *S, int m, int nt_pw, int xb, hipStream_t s);
+                            const double *H, const double *S, int m, int nt_pw, hipStream_t s);
 
 // Line-band DCGS2 step (k_band_step): update pass of step j + SpMV, tridiagonal
 // BJ(8) and dots of step j+1 in one sweep over x-lines of L rows (SELL-64 uniform width 5, coded
@@ -481,16 +459,16 @@ struct BandK {
     int canon;                   // with lsv: canonical rows (vtk_csr::lsv_canon), no codes read;
                                  // 2: the SpMV as straight-line code per line order
     int opt = 0;                 // kernel variant bits (vtk::Tuning::band_opt; vtk_band.hip OPT)
-    int j3 = 0;                  // opt bit 1 applies to steps j <= j3 (<= BAND_J3)
 };
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s);
 // geometry (k_band_step): a workgroup of BAND_T threads owns <= BAND_LP rows of a
 // line (one part; parts per line = band_parts), BAND_WPC workgroups per CU (LDS-bound)
 constexpr int BAND_LP = 400, BAND_T = 448, BAND_WPC = 2;
 constexpr int BAND_JV = 19;    // basis vectors staged per line (j + 1 <= 19: restart <= 20)
-// band steps j <= BAND_J3 may run three workgroups per CU (Tuning::band_opt bit 1): their LDS
-// (ring + (j + 1) staged basis rows of BAND_LP doubles) fits three times into 160 KB
-constexpr int BAND_J3 = 4;   // (instantiated up to here; beyond j = 2 the 80-VGPR cap spills)
+// band steps j <= BAND_J3 run three workgroups per CU (Tuning::band_opt bit 1): their LDS (ring +
+// (j + 1) staged basis rows of BAND_LP doubles) fits three times into 160 KB, and their registers
+// the 80-VGPR cap (j = 3 / 4 fit too since the x update is inline, but measured within noise)
+constexpr int BAND_J3 = 2;
 // vectors per ghost line and step of the distributed band step: v_{j-1} (v_0 at j = 0), w_j
 constexpr int BAND_GHOST_VECS = 2;
 hipError_t launch_band_check_dist(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int lblk, int *bad,
@@ -527,46 +505,21 @@ hipError_t launch_lsv_spmv(const uint32_t *pk, const int32_t *dict, const double
 // canonical order; D and tab written here
 hipError_t launch_grid4_build(const int32_t *indptr, const int32_t *indices, const void *data, int fp32, int64_t n,
                               const Grid4 &g, double *tab, void *D, int *bad, hipStream_t s);
-// Line-path DCGS2 update pass of step j fused with the next step's table SpMV (k_line_sweep,
-// one rank, canonical line-separable rows): v_j -> V[j], p_{j+1} -> p_out, y = A p_{j+1} (y null:
-// no SpMV, the cycle's last step), the x update when the step stopped the cycle (st->xup_tag == j).
-// p_j is read from p_in (V[0] at j = 0), never from V[j]: the halo lines another workgroup
-// recomputes stay readable while V[j] is overwritten.
-struct LineSweepK {
-    double *V;
-    int64_t ld;
-    int j, m;
-    const double *p_in;
-    double *p_out;
-    const double *w;
-    const DcCoef *cf;
-    const GmresState *st;
-    double *x;
-    const double *H, *S;
-    const double *lsv;
-    double *y;
-    int n, L, H_parts;
-};
-hipError_t launch_line_sweep(const LineSweepK &a, int ranges, hipStream_t s);
 // w = M^-1 A x for 4D grid rows with x staged through LDS (k_g4_ring): the tridiagonal BJ(8) of
 // m = mtri; about wgs workgroups, each a contiguous range of 256-row groups; halo != null: across
 // ranks (g.lblk the left plane's halo block).  Bit-identical to the SELL launch.  dots != null:
-// DCGS2 step dots->j fused in (x = V[j], mode 1; mode 2 the j = 0 dots alone) or the cycle-start
-// residual (mode 3, w = M^-1 (b - A x)); partials per workgroup (at most GMAX workgroups, the
-// count in *grid_out).
+// DCGS2 step 0's dots (mode 2: |p|^2, p.w, |w|^2) or the cycle-start residual (mode 3, w = M^-1
+// (b - A x)); partials per workgroup (at most GMAX workgroups, the count in *grid_out).
 struct G4Dots {
-    int mode = 1;                  // 1: step j's dots; 2: step 0's dots; 3: cycle-start residual
-    const double *V = nullptr;
-    int64_t ld = 0;
-    int j = 0;
-    double *part = nullptr;        // modes 1, 2: the dots partials (launch_dc_dots' layout)
+    int mode = 2;                  // 2: step 0's dots; 3: cycle-start residual
+    double *part = nullptr;        // mode 2: the dots partials (launch_dc_dots' layout)
     const double *b = nullptr;     // mode 3: the right-hand side; |r|^2, |w|^2 partials
     double *p0 = nullptr, *p1 = nullptr;
     int part_off = 0;              // the launch's first partial slot (split launches side by side)
 };
 // g_lo, g_hi: the group range (GR-row groups; -1: all), per: groups per workgroup (0: from wgs)
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
-                          int fp32, int wgs, int pd, int xcd, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
+                          int fp32, int wgs, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
                           int col, hipStream_t s, int g_lo = 0, int g_hi = -1, int per = 0);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);

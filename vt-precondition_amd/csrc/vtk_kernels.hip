@@ -174,9 +174,6 @@ __device__ __forceinline__ void dc_write(const DcAcc &d, int j, double *red, dou
 // lanes of the wave call it (the BJ groups exchange values by shuffles); act = a real row.
 // Returns the value written (w for the DCGS2 dots).
 // TRIM: the tridiagonal solve from m and the row's sub/sup (SELL); else from l | m | g.
-#ifndef VTK_DC_NTSTORE
-#define VTK_DC_NTSTORE 1   // w streamed out with non-temporal stores (DC; A/B: fused 593 -> 582 us)
-#endif
 template <typename VT, bool HALO, int EPI, int BS, bool TRI, bool TRIM = false>
 __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double s, int row, bool act, int lane,
                                                double &acc0, double &acc1, double sub = 0.0, double sup = 0.0,
@@ -220,7 +217,7 @@ __device__ __forceinline__ double row_epilogue(const SpmvK<VT, HALO> &a, double 
         }
         if (act) {
             if (store) {
-                if constexpr (DC && VTK_DC_NTSTORE) __builtin_nontemporal_store(z, a.y + row);
+                if constexpr (DC) __builtin_nontemporal_store(z, a.y + row);   // (A/B: fused 593 -> 582 us)
                 else st_nt<2>(a.y + row, z);
             }
             if constexpr (EPI == EPI_RESID_PREC) {
@@ -372,89 +369,31 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // register vectors at 3 waves/SIMD (-2 %), k >= 10 handed to k_dc_dots (-3 %).
 // ------------------------------------------------------------------------------------------
 
-#ifndef VTK_DC_KB
-#define VTK_DC_KB 4
-#endif
-#ifndef VTK_DC_JB
-#define VTK_DC_JB 10
-#endif
-#ifndef VTK_VAL_EARLY
-#define VTK_VAL_EARLY 1
-#endif
-#ifndef VTK_SCALAR_Q
-#define VTK_SCALAR_Q 1
-#endif
-#ifndef VTK_DC_PSW
-#define VTK_DC_PSW 4
-#endif
-#ifndef VTK_DC_HOIST
-#define VTK_DC_HOIST 1
-#endif
-#ifndef VTK_DC_WLATE
-#define VTK_DC_WLATE 0
-#endif
-#ifndef VTK_EPI_HOIST
-#define VTK_EPI_HOIST 1   // RESID / PREC / RESID_PREC: the row's m, b, v0 loaded ahead of the SpMV
-#endif
-#ifndef VTK_SELL_UNIFORM
-#define VTK_SELL_UNIFORM 1   // uniform-width SELL copies skip the offset loads (A/B: fused -1.7 %, residual -6 %)
-#endif
-#ifndef VTK_WORD_EARLY
-#define VTK_WORD_EARLY 1   // first code word loaded with the dictionary (A/B: fused -1 %, residual -6 %)
-#endif
-#ifndef VTK_DC_VPRE
-#define VTK_DC_VPRE 0   // first basis batch loaded ahead of the SpMV (r01: -0.3 %..-0.6 % time; with the compile-time-width path +1 %: off)
-#endif
-#ifndef VTK_SELL_SWZ
-#define VTK_SELL_SWZ 0   // XCD-aware group order (xcd_swizzle)
-#endif
+constexpr int DC_KB = 4;   // basis vectors per load batch (fused DC step)
+constexpr int DC_JB = 10;   // basis vectors with per-lane register accumulators (fused DC step)
+constexpr int DC_PSW = 4;   // entries per load batch of the fused DC step (runtime widths)
 // compile-time chunk width of the uniform-width SELL copies the stencil operators produce (2D
 // Vlasov: 5, 4D: 9); 0 = the runtime-width loop
-#ifndef VTK_SELL_WU
-#define VTK_SELL_WU 1
-#endif
-#ifndef VTK_DC_JB9
-#define VTK_DC_JB9 VTK_DC_JB
-#endif
-#ifndef VTK_DC_VPRE9
-#define VTK_DC_VPRE9 0   // C4 fused step: 1577 -> 1392 us without the early basis batch (spill 72 -> 20 B)
-#endif
-#ifndef VTK_DC_PSW9
-#define VTK_DC_PSW9 9   // DC load batch at width 9 (C4)
-#endif
-#ifndef VTK_SELL_PIPE
-#define VTK_SELL_PIPE 0    // fused DC step, rows <= 8 wide (C3: 536 -> 541 us with it: off)
-#endif
-#ifndef VTK_SELL_PIPE9
-#define VTK_SELL_PIPE9 0   // fused DC step, 9-wide rows (C4: 104 B spill, 1442 -> 1935 us: off)
-#endif
-#ifndef VTK_SELL_PIPEP
-#define VTK_SELL_PIPEP 0   // plain / other epilogues (C4 plain 695 -> 704-712 us with it: off)
-#endif
-#ifndef VTK_GATHER_UNCOND
-#define VTK_GATHER_UNCOND 1
-#endif
-#ifndef VTK_SELL_WPE
-#define VTK_SELL_WPE 4   // minimum waves/SIMD the SELL kernels are register-limited to
-#endif
+constexpr int DC_JB9 = 10;   // ... at width 9 (C4)
+constexpr int DC_PSW9 = 9;   // DC load batch at width 9 (C4)
+constexpr int SELL_WPE = 4;   // minimum waves/SIMD the SELL kernels are register-limited to
 // WU > 0: every chunk is WU entries wide (Sell::uniform_w == WU, checked by the launch): the
 // chunk's code words are all issued with its dictionary and the entry loop has compile-time
 // bounds, so a row wider than one code word (C4: 9 entries) costs no extra dependent round trip
 // for its second word and no batch boundary at the word edge.
 // VAR bit 0 (plain SpMV): padding slots branch around their gather instead of gathering the
-// lane's own row (VTK_GATHER_UNCOND, which the 9-wide C4 rows want)
+// lane's own row (the unconditional gather the 9-wide C4 rows want)
 template <typename VT, bool HALO, int EPI, int BS, bool TRI = false, int PSWT = 0, int WU = 0, int VAR = 0>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE))) void k_sell(SpmvK<VT, HALO> a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SELL_WPE))) void k_sell(SpmvK<VT, HALO> a) {
     // entries per load batch (DC: registers; PSWT: a row length the launch picked; WU without
     // PSWT: the whole row in one batch)
-    constexpr int PSW = PSWT > 0 ? PSWT : (WU > 0 ? WU : (EPI == EPI_PREC_DC ? VTK_DC_PSW : 8));
-    constexpr int KB = VTK_DC_KB;   // basis vectors per load batch (DC)
+    constexpr int PSW = PSWT > 0 ? PSWT : (WU > 0 ? WU : (EPI == EPI_PREC_DC ? DC_PSW : 8));
+    constexpr int KB = DC_KB;   // basis vectors per load batch (DC)
     // basis vectors with per-lane register accumulators (DC; the 9-wide rows hold more operands)
-    constexpr int JB = WU > 8 ? VTK_DC_JB9 : VTK_DC_JB;
+    constexpr int JB = WU > 8 ? DC_JB9 : DC_JB;
     constexpr bool DC = EPI == EPI_PREC_DC;
-    constexpr bool HOIST = DC && VTK_DC_HOIST;
-    constexpr bool HOISTE = !DC && EPI != EPI_PLAIN && VTK_EPI_HOIST;   // the other epilogues
-    constexpr bool WLATE = DC && VTK_DC_WLATE;
+    constexpr bool HOIST = DC;
+    constexpr bool HOISTE = !DC && EPI != EPI_PLAIN;   // the other epilogues (residual: -13 %)
     constexpr int NQW = 2 * DC_MAXJ + 3;      // per-wave partial record (DC)
     __shared__ double stage[(NT / 64) * NQW];
     __shared__ double red[NT / 64];
@@ -467,45 +406,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
 #pragma unroll
         for (int k = 0; k < JB; ++k) { as_[k] = 0.0; az_[k] = 0.0; }
     }
-    const int t0 = (VTK_SELL_SWZ || a.swz) ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    // PIPE (compile-time widths): the next chunk's code words, dictionary, values and own-row
-    // operands are loaded while this chunk's gathers are in flight -- issued right after them,
-    // so waiting for the gathers does not wait for the prefetch -- and consumed one iteration
-    // later: one dependent memory round trip less per chunk.
-    constexpr bool PIPE = WU > 0 && (DC ? (WU > 8 ? VTK_SELL_PIPE9 : VTK_SELL_PIPE) : VTK_SELL_PIPEP);
-    constexpr int NWDP = WU > 0 ? (WU + 7) / 8 : 1;
-    [[maybe_unused]] VT pf_d[PIPE ? WU : 1];
-    [[maybe_unused]] uint32_t pf_wd[NWDP];
-    [[maybe_unused]] int pf_dv = 0;
-    [[maybe_unused]] double pf_m = 1.0, pf_p = 0.0;
-    auto prefetch = [&](int tt) {
-        if constexpr (PIPE) {
-            if (tt >= a.ngroups) return;   // wave-uniform
-            const int gg = a.group_list ? a.group_list[tt] : tt;
-            const int qq = VTK_SCALAR_Q ? __builtin_amdgcn_readfirstlane(4 * gg + wv) : 4 * gg + wv;
-            const int rr = 64 * qq + lane;
-            if (64 * qq >= a.n_local) return;
-            const VT *vv = a.sell_val + (int64_t)qq * 64 * WU + lane;
-            if (a.pk) {
-                const uint32_t *pw = a.pk + (int64_t)qq * 64 * NWDP + lane;
-#pragma unroll
-                for (int u = 0; u < NWDP; ++u) pf_wd[u] = __builtin_nontemporal_load(pw + u * 64);
-                pf_dv = lane < 16 ? a.dict[(int64_t)qq * 16 + lane] : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < WU; ++k) pf_d[k] = __builtin_nontemporal_load(vv + k * 64);
-            if constexpr (HOIST) {
-                if (rr < a.n_local) {
-                    if constexpr (TRI && BS > 0) pf_m = ld_nt<1>(a.tri + a.tri_ld + rr);
-                    pf_p = a.x[rr];
-                }
-            }
-        }
-    };
-    if constexpr (PIPE) prefetch(t0);
+    const int t0 = a.swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     for (int t = t0; t < a.ngroups; t += gridDim.x) {
         const int g = a.group_list ? a.group_list[t] : t;
-        const int q = VTK_SCALAR_Q ? __builtin_amdgcn_readfirstlane(4 * g + wv) : 4 * g + wv;
+        const int q = __builtin_amdgcn_readfirstlane(4 * g + wv);
         const int row = 64 * q + lane;
         const bool act = row < a.n_local;
         double s = 0.0;
@@ -515,21 +419,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // HOIST: the row's own operands (BJ factor m, p, b, v0) issued ahead of the CSR loads,
         // so the epilogue does not wait a memory round trip per chunk (EPI_PREC: 352 -> ... us)
         double mrow = 1.0, pv = 0.0, bv = 0.0, v0v = 0.0;
-        [[maybe_unused]] VT cur_d[PIPE ? WU : 1];
-        [[maybe_unused]] uint32_t cur_wd[NWDP];
-        [[maybe_unused]] int cur_dv = 0;
-        if constexpr (PIPE) {
-#pragma unroll
-            for (int k = 0; k < WU; ++k) cur_d[k] = pf_d[k];
-#pragma unroll
-            for (int u = 0; u < NWDP; ++u) cur_wd[u] = pf_wd[u];
-            cur_dv = pf_dv;
-            if constexpr (HOIST) {
-                mrow = act ? pf_m : 1.0;
-                pv = act ? pf_p : 0.0;
-            }
-        }
-        if constexpr (HOIST && !PIPE) {
+        if constexpr (HOIST) {
             if (act) {
                 if constexpr (TRIM) mrow = ld_nt<1>(a.tri + a.tri_ld + row);
                 pv = a.x[row];
@@ -543,15 +433,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 }
             }
         }
-        // VPRE: the first batch of basis rows is loaded before the SpMV (no dependence on it),
-        // in flight during the gather chain
-        constexpr bool VPRE = DC && VTK_DC_VPRE && (WU <= 8 || VTK_DC_VPRE9);
-        [[maybe_unused]] double vpre[VPRE ? KB : 1];
-        if constexpr (VPRE) {
-#pragma unroll
-            for (int u = 0; u < KB; ++u)
-                vpre[u] = (u < JB && u < a.j && act) ? __builtin_nontemporal_load(a.V + row + (size_t)u * a.ld) : 0.0;
-        }
         // products of one batch, summed serially in stored order (padding skipped)
         auto batch = [&](const auto &c, const auto &d, auto mid) {
             constexpr int NB = sizeof(c) / sizeof(c[0]);
@@ -562,7 +443,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 // entry) instead of branching around the load: the gathers issue back to back
                 // with no exec-mask blocks.  (x[0] for every padding slot measured 1.6x slower on
                 // C4: one hot L2 line for the whole chip.)
-                if constexpr (VTK_GATHER_UNCOND && !(VAR & 1)) xv[u] = xload(a, c[u] >= 0 ? c[u] : (act ? row : 0));
+                if constexpr (!(VAR & 1)) xv[u] = xload(a, c[u] >= 0 ? c[u] : (act ? row : 0));
                 else xv[u] = c[u] >= 0 ? xload(a, c[u]) : 0.0;
             }
             mid();
@@ -583,8 +464,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
         // round trips; the same entries in the same order as the SELL copy (canon_row)
         // (not in the plain SpMV: vtk_spmv, the measured standalone SpMV, never has lsv, and the
         // extra path cost its loop 249 -> 372 us on C3 through code shape alone)
-        constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && !PIPE && EPI != EPI_PLAIN;
-        constexpr bool G4_OK = (WU == 0 || WU == 9) && !PIPE && EPI != EPI_PLAIN && (VAR & 2) == 0;
+        constexpr bool CANON_OK = std::is_same<VT, double>::value && (WU == 0 || WU == 5) && EPI != EPI_PLAIN;
+        constexpr bool G4_OK = (WU == 0 || WU == 9) && EPI != EPI_PLAIN && (VAR & 2) == 0;
         // the line-separable tables are a solver-launch form: compiled out of the plain SpMV (its
         // per-entry value selection cost the measured kernel 222 -> 242 us on C3)
         constexpr bool LSV_OK = EPI != EPI_PLAIN;
@@ -700,25 +581,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 int dv = 0;
                 bool wide = true;   // wave-uniform
                 VT dall[WU];   // raw (fp32 values: one VGPR each until used)
-                if constexpr (PIPE) {
+                if (a.pk) {
+                    const uint32_t *pw = a.pk + (int64_t)q * 64 * NWD + lane;
 #pragma unroll
-                    for (int u = 0; u < NWD; ++u) wd[u] = cur_wd[u];
-                    dv = cur_dv;
+                    for (int u = 0; u < NWD; ++u) wd[u] = __builtin_nontemporal_load(pw + u * 64);
+                    dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
+                }
+                // the row's values do not depend on the column form: issued with the codes and
+                // the dictionary, before the form test waits for the dictionary
+                if (!(LSV_OK && a.lsv)) {
 #pragma unroll
-                    for (int k = 0; k < WU; ++k) dall[k] = cur_d[k];
-                } else {
-                    if (a.pk) {
-                        const uint32_t *pw = a.pk + (int64_t)q * 64 * NWD + lane;
-#pragma unroll
-                        for (int u = 0; u < NWD; ++u) wd[u] = __builtin_nontemporal_load(pw + u * 64);
-                        dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
-                    }
-                    // the row's values do not depend on the column form: issued with the codes
-                    // and the dictionary, before the form test waits for the dictionary
-                    if (!(LSV_OK && a.lsv)) {
-#pragma unroll
-                        for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
-                    }
+                    for (int k = 0; k < WU; ++k) dall[k] = __builtin_nontemporal_load(vv + k * 64);
                 }
                 // line-separable values: the row's diagonal, line and position
                 double lsv_d = 0.0;
@@ -758,15 +631,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                             }
                             d[u] = (LSV_OK && a.lsv) ? (c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0) : (double)dall[k];
                         }
-                        batch(c, d, [&] {
-                            if constexpr (PIPE) {
-                                if (k0 == 0) {
-                                    __builtin_amdgcn_sched_barrier(0);
-                                    prefetch(t + (int)gridDim.x);
-                                    __builtin_amdgcn_sched_barrier(0);
-                                }
-                            }
-                        });
+                        batch(c, d, [] {});
                     }
                 };
                 if (wide) entries(std::true_type{});
@@ -785,7 +650,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
             // has its pk words, wide or not), not after the wide test has seen the dictionary
             const uint32_t *pw = a.pk ? a.pk + (a.sell_uw ? (int64_t)q * 64 * ((a.sell_uw + 7) / 8) : a.pk_off[q]) + lane
                                       : nullptr;
-            const uint32_t word0 = (VTK_WORD_EARLY && a.pk && w > 0) ? __builtin_nontemporal_load(pw) : 0u;
+            const uint32_t word0 = (a.pk && w > 0) ? __builtin_nontemporal_load(pw) : 0u;
             if (a.pk) {   // the chunk's dictionary: one 64-B load by lanes 0..15
                 dv = lane < 16 ? a.dict[(int64_t)q * 16 + lane] : 0;
                 wide = __shfl(dv, 15, 64) != 0;
@@ -804,7 +669,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
             }
             for (int k0 = 0; k0 < w; k0 += 8) {
                 const uint32_t word = wide ? 0u
-                                           : ((VTK_WORD_EARLY && k0 == 0) ? word0
+                                           : ((k0 == 0) ? word0
                                                                           : __builtin_nontemporal_load(pw + (k0 >> 3) * 64));
 #pragma unroll
                 for (int h = 0; h < 8; h += PSW) {
@@ -829,7 +694,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
 #pragma unroll
                     for (int u = 0; u < PSW; ++u) {
                         if (LSV_OK && a.lsv) d[u] = c[u] >= 0 ? lsv_value(a, row, c[u], lsv_d, lsv_x, lsv_v) : 0.0;
-                        else d[u] = (VTK_VAL_EARLY ? (h + u < 8 && k0 + h + u < w) : c[u] >= 0)
+                        else d[u] = (h + u < 8 && k0 + h + u < w)
                                         ? (double)__builtin_nontemporal_load(vv + (k0 + h + u) * 64) : 0.0;
                     }
                     batch(c, d, [] {});
@@ -837,7 +702,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
             }
         }
         const double z = row_epilogue<VT, HALO, EPI, BS, TRI, TRIM>(a, s, row, act, lane, acc0, acc1, sub, sup,
-                                                                    (HOIST || HOISTE) && TRIM, mrow, !WLATE,
+                                                                    (HOIST || HOISTE) && TRIM, mrow, true,
                                                                     HOISTE, bv, v0v);
         if constexpr (DC) {
             if constexpr (!HOIST) pv = act ? a.x[row] : 0.0;   // p_j (= the SpMV input) on this row
@@ -851,12 +716,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                 double v[KB];
 #pragma unroll
                 for (int u = 0; u < KB; ++u) {
-                    if constexpr (VPRE) {
-                        if (k0 == 0) {
-                            v[u] = vpre[u];
-                            continue;
-                        }
-                    }
                     v[u] = (k0 + u < JB && k0 + u < a.j && act)
                                ? __builtin_nontemporal_load(vb + (size_t)(k0 + u) * a.ld) : 0.0;
                 }
@@ -883,9 +742,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VTK_SELL_WPE
                         }
                     }
                 }
-            }
-            if constexpr (WLATE) {
-                if (act) a.y[row] = z;
             }
         }
     }
@@ -1072,7 +928,7 @@ size_t sell_scan_bytes(int64_t n) {
 // workgroups of the plain SELL SpMV (no partials: free of GMAX); vtk::Tuning::plain_grid
 static inline int plain_grid(const SpmvIn &in) { return in.plain_grid > 0 ? in.plain_grid : 2 * GMAX; }
 static inline int sell_wu(const SpmvIn &in) {
-    if (!VTK_SELL_WU || !VTK_SELL_UNIFORM || !in.sell || !in.groups) return 0;
+    if (!in.sell || !in.groups) return 0;
     const int w = in.sell->uniform_w;
     return (w == 5 || w == 9) ? w : 0;
 }
@@ -1089,7 +945,7 @@ static hipError_t launch_bj_variant(const SpmvK<VT, HALO> &a, int bs, bool tri, 
     if (tri) {
         // 9-wide uniform rows (C4): the compile-time-width path (the cycle-start residual
         // kernel, 1440 us with the runtime loop)
-        if (EPI != EPI_PREC_DC && VTK_SELL_WU && sell && bs == 8 && a.sell_uw == 9) {
+        if (EPI != EPI_PREC_DC && sell && bs == 8 && a.sell_uw == 9) {
             if (a.g4.tab) hipLaunchKernelGGL((k_sell<VT, HALO, EPI, 8, true, 0, 9, 2>), g, blk, 0, s, a);
             else hipLaunchKernelGGL((k_sell<VT, HALO, EPI, 8, true, 0, 9>), g, blk, 0, s, a);
             return hipGetLastError();
@@ -1131,7 +987,7 @@ static SpmvK<VT, HALO> spmv_args(const SpmvIn &in, double *y, const double *b, c
                       sell ? static_cast<const VT *>(in.sell->d_val) : nullptr,
                       sell ? in.groups->d_list : nullptr, sell ? in.groups->count : 0,
                       sell ? in.sell->d_pk : nullptr, sell ? in.sell->d_pkoff : nullptr,
-                      sell ? in.sell->d_dict : nullptr, sell && VTK_SELL_UNIFORM ? in.sell->uniform_w : 0,
+                      sell ? in.sell->d_dict : nullptr, sell ? in.sell->uniform_w : 0,
                       sell && !std::is_same<VT, float>::value ? in.lsv : nullptr, in.lsv_L, in.lsv_lblk, in.lsv_xord,
                       sell && !std::is_same<VT, float>::value && in.lsv ? in.lsv_canon : 0, in.swz,
                       sell ? in.g4 : Grid4{}};
@@ -1189,8 +1045,8 @@ static hipError_t spmv_dc_dispatch(const SpmvIn &in, double *w, const BjOp &bj, 
         return hipGetLastError();
     }
     if (sell && bj.tri && bs == 8 && wu == 9) {
-        if (a.g4.tab) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, VTK_DC_PSW9, 9, 2>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
-        else hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, VTK_DC_PSW9, 9>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        if (a.g4.tab) hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, DC_PSW9, 9, 2>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
+        else hipLaunchKernelGGL((k_sell<VT, HALO, EPI_PREC_DC, 8, true, DC_PSW9, 9>), dim3(spmv_grid(in)), dim3(NT), 0, s, a);
         return hipGetLastError();
     }
     if (sell && bj.tri && bs == 8 && in.sell->nch > 0 && in.sell->entries <= in.sell->nch * 64 * 5) {
@@ -2232,7 +2088,6 @@ hipError_t launch_scale0(Red p, double *v0, int64_t n, double *S, int m, GmresSt
 // (iterative.py:799-814).  Workgroup-redundant triangular solve on lane 0, into LDS.
 // ------------------------------------------------------------------------------------------
 
-template <int XB>
 __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, const double *__restrict__ S,
                                                 const double *__restrict__ V, int64_t ld,
                                                 double *__restrict__ x, int64_t n, int m,
@@ -2246,19 +2101,7 @@ __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, co
     for (int64_t i = 2 * ((int64_t)blockIdx.x * NT + threadIdx.x); i < n; i += stride) {
         if (i + 1 < n) {
             double ax = 0.0, ay = 0.0;
-            int k = 0;   // XB > 1: basis rows loaded in batches (sums in ascending k)
-            if constexpr (XB > 1)
-            for (; k + XB <= col + 1; k += XB) {
-                d2v v[XB];
-#pragma unroll
-                for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
-#pragma unroll
-                for (int u = 0; u < XB; ++u) {
-                    ax += ys[k + u] * v[u].x;
-                    ay += ys[k + u] * v[u].y;
-                }
-            }
-            for (; k <= col; ++k) {
+            for (int k = 0; k <= col; ++k) {
                 const d2v v = ldnt2(V + (size_t)k * ld + i);
                 ax += ys[k] * v.x;
                 ay += ys[k] * v.y;
@@ -2276,9 +2119,8 @@ __global__ __launch_bounds__(NT) void k_xupdate(const double *__restrict__ H, co
 }
 
 hipError_t launch_xupdate(const double *H, const double *S, const double *V, int64_t ld, double *x,
-                          int64_t n, int m, const GmresState *st, int grid, int xb, hipStream_t s) {
-    if (xb > 0) hipLaunchKernelGGL(k_xupdate<8>, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n, m, st);
-    else hipLaunchKernelGGL(k_xupdate<0>, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n, m, st);
+                          int64_t n, int m, const GmresState *st, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_xupdate, dim3(grid), dim3(NT), (m + 1) * sizeof(double), s, H, S, V, ld, x, n, m, st);
     return hipGetLastError();
 }
 
@@ -2441,76 +2283,6 @@ hipError_t launch_remap_cols(int32_t *indices, int64_t nnz, int64_t row_begin, i
 // column j (c' = (e - H_j s)/r, e = [z; (beta - s.z)/r]) and nu_{j+1} = sqrt(gamma - e.e)/r;
 // ONE update pass writes v_j and p_{j+1} = (w - [V_j v_j] e) / (r nu).  Derivation: DESIGN.md.
 // ------------------------------------------------------------------------------------------
-#ifndef VTK_DOTS_WAVESPLIT
-#define VTK_DOTS_WAVESPLIT 0   // 1: the basis split over the waves (k_dc_dots) instead of rows
-#endif
-__global__ __launch_bounds__(NT) void k_dc_dots(const double *__restrict__ V, int64_t ld, int j,
-                                                const double *__restrict__ w, int64_t n, double *part,
-                                                const int *stop_col, int col) {
-    constexpr int KPW = DC_MAXJ / (NT / 64);   // basis vectors per wave
-    __shared__ double red[DC_NQ];
-    if (stopped(stop_col, col)) return;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const double *p = V + (size_t)j * ld;
-    double as[KPW], az[KPW];
-#pragma unroll
-    for (int u = 0; u < KPW; ++u) { as[u] = 0.0; az[u] = 0.0; }
-    double aa = 0.0, ab = 0.0, ag = 0.0;
-    const int64_t stride = 2 * (int64_t)gridDim.x * 64;
-    for (int64_t i = 2 * ((int64_t)blockIdx.x * 64 + lane); i < n; i += stride) {
-        const bool two = i + 1 < n;
-        double2 pv, wv2;
-        if (two) {
-            pv = *reinterpret_cast<const double2 *>(p + i);
-            wv2 = w ? *reinterpret_cast<const double2 *>(w + i) : make_double2(0.0, 0.0);
-        } else {
-            pv = make_double2(p[i], 0.0);
-            wv2 = make_double2(w ? w[i] : 0.0, 0.0);
-        }
-#pragma unroll
-        for (int u = 0; u < KPW; ++u) {
-            const int k = wv + u * (NT / 64);
-            if (k < j) {
-                const double *vk = V + (size_t)k * ld + i;
-                const double2 v = two ? *reinterpret_cast<const double2 *>(vk) : make_double2(vk[0], 0.0);
-                as[u] += v.x * pv.x;
-                as[u] += v.y * pv.y;
-                if (w) {
-                    az[u] += v.x * wv2.x;
-                    az[u] += v.y * wv2.y;
-                }
-            }
-        }
-        if (wv == 0) {
-            aa += pv.x * pv.x;
-            aa += pv.y * pv.y;
-            if (w) {
-                ab += pv.x * wv2.x;
-                ab += pv.y * wv2.y;
-                ag += wv2.x * wv2.x;
-                ag += wv2.y * wv2.y;
-            }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < KPW; ++u) {
-        const int k = wv + u * (NT / 64);
-        const double ts = wave_sum(as[u]);
-        const double tz = wave_sum(az[u]);
-        if (lane == 0 && k < j) { red[k] = ts; red[DC_MAXJ + k] = tz; }
-    }
-    {
-        const double t0 = wave_sum(aa), t1 = wave_sum(ab), t2 = wave_sum(ag);
-        if (wv == 0 && lane == 0) { red[2 * DC_MAXJ] = t0; red[2 * DC_MAXJ + 1] = t1; red[2 * DC_MAXJ + 2] = t2; }
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < DC_NQ; q += NT) {
-        const bool used = q < j || (q >= DC_MAXJ && q < DC_MAXJ + j && w) || q == 2 * DC_MAXJ ||
-                          (w && q > 2 * DC_MAXJ);
-        if (used) part[(size_t)q * GMAX + blockIdx.x] = red[q];
-    }
-}
-
 // The same dots with every thread owning row pairs (as k_dc_update): p and w are read once per
 // row instead of once per wave, every basis vector streams through 16-B non-temporal loads and
 // the thread keeps JM >= j accumulators per quantity.  Same partial layout.
@@ -2590,8 +2362,7 @@ hipError_t launch_dc_dots(const double *V, int64_t ld, int j, const double *w, i
                           int grid, const int *stop_col, int col, hipStream_t s) {
     if (j > DC_MAXJ) return hipErrorInvalidValue;
     const dim3 g(grid), b(NT);
-    if (VTK_DOTS_WAVESPLIT) hipLaunchKernelGGL(k_dc_dots, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
-    else if (j <= 8) hipLaunchKernelGGL(k_dc_dots_rows<8>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
+    if (j <= 8) hipLaunchKernelGGL(k_dc_dots_rows<8>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
     else if (j <= 16) hipLaunchKernelGGL(k_dc_dots_rows<16>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
     else if (j <= 24) hipLaunchKernelGGL(k_dc_dots_rows<24>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
     else hipLaunchKernelGGL(k_dc_dots_rows<DC_MAXJ>, g, b, 0, s, V, ld, j, w, n, part, stop_col, col);
@@ -2639,16 +2410,15 @@ hipError_t launch_dc_scalar(const double *part, int cnt, const double *scal, int
 
 // NTPW: p_j and w loaded non-temporal (A/B: +2 % on the unfused (line) path, -1 % after the
 // fused BJ step, whose w the update re-reads warm)
-// XB > 0: the basis rows loaded in batches of XB (the same sums in the same order)
-template <bool NTPW, int XB>
+template <bool NTPW>
 __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_t ld, int j,
                                                   const double *__restrict__ w, int64_t n,
                                                   const DcCoef *cf, const GmresState *st, double *x,
                                                   const double *H, const double *S, int m) {
     __shared__ double cs[DC_MAXJ], ce[DC_MAXJ + 1];
     __shared__ double rinv_s, q_s;
-    if (VTK_XUP_FUSED && __builtin_nontemporal_load(&st->xup_tag) == j) {
-        dc_xupdate_body<XB>(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m, nullptr);
+    if (__builtin_nontemporal_load(&st->xup_tag) == j) {   // the cycle's x update (one basis read less)
+        dc_xupdate_body<0>(V, ld, j, __builtin_nontemporal_load(&st->stop_col), n, cf, x, H, S, m, nullptr);
         return;
     }
     if (stopped(&st->stop_col, j)) return;
@@ -2681,30 +2451,18 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
                 t.x = t.x - ek * v.x;
                 t.y = t.y - ek * v.y;
             };
-            int k = 0;
-            if constexpr (XB > 0) {
-                for (; k + XB <= j; k += XB) {
-                    d2v v[XB];
-#pragma unroll
-                    for (int u = 0; u < XB; ++u) v[u] = ldnt2(V + (size_t)(k + u) * ld + i);
-#pragma unroll
-                    for (int u = 0; u < XB; ++u) acc1(k + u, v[u]);
-                }
-            }
-            for (; k < j; ++k) acc1(k, ldnt2(V + (size_t)k * ld + i));
+            for (int k = 0; k < j; ++k) acc1(k, ldnt2(V + (size_t)k * ld + i));
             double2 vj = p;
             if (j >= 1) {
                 vj.x = a.x * rinv;
                 vj.y = a.y * rinv;
-                if constexpr (VTK_UPD_NT >= 1) __builtin_nontemporal_store(d2v{vj.x, vj.y}, reinterpret_cast<d2v *>(pj + i));
-                else *reinterpret_cast<double2 *>(pj + i) = vj;
+                __builtin_nontemporal_store(d2v{vj.x, vj.y}, reinterpret_cast<d2v *>(pj + i));
             }
             t.x = t.x - ej * vj.x;
             t.y = t.y - ej * vj.y;
             t.x = t.x * q;
             t.y = t.y * q;
-            if constexpr (VTK_UPD_NT >= 2) __builtin_nontemporal_store(d2v{t.x, t.y}, reinterpret_cast<d2v *>(pn + i));
-            else *reinterpret_cast<double2 *>(pn + i) = t;
+            __builtin_nontemporal_store(d2v{t.x, t.y}, reinterpret_cast<d2v *>(pn + i));
         } else {
             const double p = pj[i];
             double a = p, t = w[i];
@@ -2723,17 +2481,9 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
 
 hipError_t launch_dc_update(double *V, int64_t ld, int j, const double *w, int64_t n, const DcCoef *cf,
                             int grid, const GmresState *st, double *x, const double *H, const double *S, int m,
-                            int nt_pw, int xb, hipStream_t s) {
-#ifdef VTK_UPD_NTPW_FORCE
-    nt_pw = VTK_UPD_NTPW_FORCE;
-#endif
-    if (xb > 0) {
-        if (nt_pw) hipLaunchKernelGGL((k_dc_update<true, 8>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
-        else hipLaunchKernelGGL((k_dc_update<false, 8>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
-    } else {
-        if (nt_pw) hipLaunchKernelGGL((k_dc_update<true, 0>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
-        else hipLaunchKernelGGL((k_dc_update<false, 0>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
-    }
+                            int nt_pw, hipStream_t s) {
+    if (nt_pw) hipLaunchKernelGGL((k_dc_update<true>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
+    else hipLaunchKernelGGL((k_dc_update<false>), dim3(grid), dim3(NT), 0, s, V, ld, j, w, n, cf, st, x, H, S, m);
     return hipGetLastError();
 }
 
