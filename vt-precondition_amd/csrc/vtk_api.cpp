@@ -1192,6 +1192,10 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // line-separable values in the band step (tuning band_lsv 0: the SELL values)
     const bool band_lsv = band && s.A->d_lsv && c->tune.band_lsv;
     const bool band_canon = c->tune.band_canon != 0;       // 0: read the codes anyway (A/B)
+    // the band step's variant bits exist for the one-rank instantiation (line-separable values,
+    // canonical rows, no ghost lines; launch_band_one_rank): every other launch, and the partial
+    // count its successor reads, takes the base grid
+    const int band_opt = band_lsv && s.A->lsv_canon && band_canon && !s.ghost ? c->tune.band_opt : 0;
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)
     const double b_band = band_lsv ? (s.A->lsv_canon && band_canon
@@ -1210,7 +1214,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         double *const wb[3] = {s.w, s.tmp, s.w3};
         double *w_cur = band ? wb[j % 3] : s.w;
         if (band && j > 0) {
-            cnt = s.band_grid(j - 1, s.ghost ? 0 : c->tune.band_opt);
+            cnt = s.band_grid(j - 1, band_opt);
         } else if (fused && band && j == 0 && cyc_ring_ok(c, s.A, s.M, true)) {
             // step 0 of a band cycle through the x-line ring (x = v_0; the j = 0 dots only);
             // across ranks the two halo lines first (12.8 KB at C3)
@@ -1386,7 +1390,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.xord = s.A->band_xord;
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
             a.canon = band_lsv && s.A->lsv_canon && band_canon ? 2 : 0;   // 2: the straight-line SpMV per line order
-            a.opt = s.ghost ? 0 : c->tune.band_opt;   // variants exist for the one-rank instantiation
+            a.opt = band_opt;
             HIPCHK(c, launch_band_step(a, s.band_grid(j, a.opt), s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
