@@ -18,5 +18,7 @@ slabs) for cp in C3:8 C3:4 C3:2 C4:8; do c=${cp%%:*}; p=${cp##*:}
          run slab_${c}_$p 300 python bench.py --config $c --slab $p --comm-solo --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 2
          grep '^{' gpurun_out/slab_${c}_$p.log | tail -1 >> gpurun_out/slabs.jsonl; done ;;
 c4) run bench_c4 600 python bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline ;;
+pmcab) for v in ${AB_VALUES//,/ }; do k=0; for ctr in ${PMC_SETS:-FETCH_SIZE TCC_HIT_sum,TCC_MISS_sum}; do k=$((k+1))
+         run pmc_${AB_ENV}_${v}_$k 300 rocprofv3 --pmc ${ctr//,/ } -d gpurun_out/pmc_${AB_ENV}_${v}_$k -o run --output-format csv -- python tools/ab_env.py --env "$AB_ENV" --values "$v" --rounds 1 --config "${AB_CFG:-C3}" --set "${AB_SET:-}"; done; done ;;
 *) echo "unknown stage $st"; exit 2 ;;
 esac; done
