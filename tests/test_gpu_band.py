@@ -178,17 +178,19 @@ def test_band_line_separable_values_bit_identical(vk_lib, gpu, name):
     M = vk_lib.block_jacobi(A, 8)
     b = twin.rhs(p.n)
     # (cyc_ring 0: the cycle-start launches through k_sell, which sums its reductions in the same
-    # order with and without the tables; the ring form is pinned by test_cycle_ring_epilogues)
-    with gpu.tuning(cyc_ring=0):
+    # order with and without the tables; the ring form is pinned by test_cycle_ring_epilogues.
+    # band_opt 0: the one-rank variants' grid exists only with the tables and canonical rows, and
+    # the dots' partials follow the grid -- test_band_step_variants pins the variants)
+    with gpu.tuning(cyc_ring=0, band_opt=0):
         x1, i1, s1 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
-    with gpu.tuning(band_lsv=0, cyc_ring=0):
+    with gpu.tuning(band_lsv=0, cyc_ring=0, band_opt=0):
         x0, i0, s0 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     # canonical rows (the kinds' order from the row's line instead of the SELL codes) vs the codes
-    with gpu.tuning(band_canon=0, cyc_ring=0):
+    with gpu.tuning(band_canon=0, cyc_ring=0, band_opt=0):
         x2, i2, s2 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     # the cycle-start SELL launches (residual + BJ, step 0's SpMV + BJ + dots) with their columns
     # from canon_row vs the codes
-    with gpu.tuning(sell_canon=0, cyc_ring=0):
+    with gpu.tuning(sell_canon=0, cyc_ring=0, band_opt=0):
         x3, i3, s3 = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     assert s1.band == s0.band == s2.band == s3.band == 1 and i1 == i0 == i2 == i3 == 0
     assert s1.inner_iters == s0.inner_iters == s2.inner_iters == s3.inner_iters
