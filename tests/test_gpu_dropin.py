@@ -192,6 +192,9 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
                 assert np.linalg.norm(x3 - x1) / np.linalg.norm(x1) < 1e-9, (wgs, gr)
             # default: the ring split step (2048 workgroups of 512 rows)
             xd, _, sd = _solve(vk_lib, A, M, b, orth=orth)
+            with gpu.tuning(g4_fast=0):   # every wave through the general select chains
+                xg, _, sg = _solve(vk_lib, A, M, b, orth=orth)
+            assert np.array_equal(xd, xg) and sd.inner_iters == sg.inner_iters, "the inner-row sum changes the bits"
             xe, _, se = _solve(vk_lib, A, M, b, orth=orth, x0=b * 1e-3)
             xf, _, sf = _solve(vk_lib, A, M, b, orth=orth, x0=b * 1e-3)
             assert np.array_equal(xe, xf) and se.inner_iters == sf.inner_iters

@@ -81,7 +81,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"band_canon", &Tuning::band_canon}, {"band_opt", &Tuning::band_opt}, {"lsv_ring", &Tuning::lsv_ring},
     {"prof_perj", &Tuning::prof_perj}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring},
-    {"g4_gr", &Tuning::g4_gr}, {"cyc_ring", &Tuning::cyc_ring},
+    {"g4_gr", &Tuning::g4_gr}, {"g4_fast", &Tuning::g4_fast}, {"cyc_ring", &Tuning::cyc_ring},
 };
 // switches of earlier rounds whose alternative lost its A/B: an environment that
 // still sets one is told once that it no longer has an effect
@@ -1290,7 +1290,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring);
                 int grid = 0;
                 HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_gr,
-                                         dc ? &dd : nullptr, &grid, stop, j, c->stream));
+                                         dc ? &dd : nullptr, &grid, stop, j, c->stream, 0, -1, 0,
+                                         c->tune.g4_fast));
                 if (dc) cnt = grid;
             } else {
                 // across ranks: the rows [S4, n - S4) read no halo plane -- their groups run while
@@ -1311,7 +1312,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                     if (gi_hi > gi_lo)
                         HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                                  c->tune.g4_gr, dc ? &dd : nullptr, &gin, stop, j, c->stream, (int)gi_lo,
-                                                 (int)gi_hi, per));
+                                                 (int)gi_hi, per, c->tune.g4_fast));
                 }
                 if (exch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
                 {
@@ -1319,12 +1320,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                     dd.part_off = gin;
                     HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                              c->tune.g4_gr, dc ? &dd : nullptr, &gb0, stop, j, c->stream, 0,
-                                             (int)(gi_hi > gi_lo ? gi_lo : ng), per));
+                                             (int)(gi_hi > gi_lo ? gi_lo : ng), per, c->tune.g4_fast));
                     if (gi_hi > gi_lo) {
                         dd.part_off = gin + gb0;
                         HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                                  c->tune.g4_gr, dc ? &dd : nullptr, &gb1, stop, j, c->stream, (int)gi_hi,
-                                                 (int)ng, per));
+                                                 (int)ng, per, c->tune.g4_fast));
                     }
                 }
                 if (dc) cnt = gin + gb0 + gb1;
@@ -1567,7 +1568,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             int g = 0;
             HIPCHK(c, launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
                                      c->tune.g4_ring, c->tune.g4_gr, &dd, &g, nullptr,
-                                     0, c->stream));
+                                     0, c->stream, 0, -1, 0, c->tune.g4_fast));
             TRY(pad_partials(c, prr, prz, g));
             rr = reduce(c, prr, g, rc2);
             TRY(rc2);

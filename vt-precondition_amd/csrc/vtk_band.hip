@@ -844,9 +844,12 @@ template <typename VT, bool HALO, int RL, int MODE, int GR>
 __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 && RL <= 5120 ? 6 : 1))) void k_g4_ring(Grid4 g, const double *__restrict__ x, const double *__restrict__ halo,
                                                 const double *__restrict__ mtri, double *__restrict__ w, int n,
                                                 int ngroups_per_wg, int g_lo, int g_hi, G4Dots dd, const int *stop_col,
-                                                int col) {
+                                                int col, int fast) {
     constexpr bool RES = MODE == 3;
-    __shared__ double ring[RL];
+    // the ring with G4RM-slot mirrors of its ends (slot t < G4RM also at RL + t, t >= RL - G4RM
+    // also at t - RL): the +-1 and +-Nvy reads need no wrap
+    __shared__ double ring_m[G4RM + RL + G4RM];
+    double *const ring = ring_m + G4RM;
     __shared__ double tb[G4TAB];
     __shared__ double red3[3][MODE >= 2 ? GR / 64 : 1];
     double e0 = 0.0, e1 = 0.0, e2 = 0.0;   // MODE 2 / 3: the lane's sums over its rows
@@ -871,7 +874,13 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
     for (int i = tid; i < ovy + 2 * Ny; i += GR) tb[i] = g.tab[i];
     // the window's initial rows [gb GR - S3, gb GR + GR + S3), clamped to [0, n)
     for (int r = gb * GR - S3 + tid; r < gb * GR + GR + S3; r += GR)
-        if (r >= 0 && r < n) ring[r % RL] = x[r];
+        if (r >= 0 && r < n) {
+            const int t = r % RL;
+            const double v = x[r];
+            ring[t] = v;
+            if (t < G4RM) ring[RL + t] = v;
+            if (t >= RL - G4RM) ring[t - RL] = v;
+        }
     // GR in the mixed radix (Nvy, Nvx, Ny, X)
     const int a0 = GR % Nvy, q0 = GR / Nvy, a1 = q0 % Nvx, q1 = q0 / Nvx, a2 = q1 % Ny, a3 = q1 / Ny;
     struct Co {
@@ -933,11 +942,13 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
     Ld nx;
     load(gb, nx);
     int sb = (gb * GR + tid) % RL;   // ring slot of the lane's row
-    auto slot = [&](int off) {
-        int t = sb + off;
-        t += t < 0 ? RL : 0;
-        t -= t >= RL ? RL : 0;
-        return t;
+    auto slotp = [&](int off) {   // sb + off, 0 <= off < RL
+        const int t = sb + off;
+        return t >= RL ? t - RL : t;
+    };
+    auto slotm = [&](int off) {   // sb - off, 0 <= off < RL
+        const int t = sb - off;
+        return t < 0 ? t + RL : t;
     };
     __syncthreads();
     for (int gi = gb; gi < ge; ++gi) {
@@ -948,39 +959,57 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
         const int rc = act ? r : n - 1;
         const int jvy = cu.c.jvy, jvx = cu.c.jvx, iy = cu.c.iy, ix = cu.c.ix;
         const bool pvm = jvx > 0, pvp = jvx < Nvx - 1, pym = jvy > 0, pyp = jvy < Nvy - 1;
-        // in-plane neighbours from the ring (y wraps from the queue)
-        const int cym = iy == 0 ? rc + (Ny - 1) * S3 : rc - S3;
-        const int cyp = iy == Ny - 1 ? rc - (Ny - 1) * S3 : rc + S3;
-        const double xym = iy == 0 ? cu.xw : ring[slot(-S3)];
-        const double xyp = iy == Ny - 1 ? cu.xw : ring[slot(S3)];
-        const double xvm = ring[slot(-S2)], xvp = ring[slot(S2)];
-        const double xwm = ring[slot(-1)], xwp = ring[slot(1)];
+        const double xvm = ring[sb - S2], xvp = ring[sb + S2];   // (mirrored ends)
+        const double xwm = ring[sb - 1], xwp = ring[sb + 1];
         const double x0 = ring[sb];
         const int jx = min(jvx, Nvx - 1), jy = min(jvy, Nvy - 1), kx = min(ix, g.X - 1), ky = min(iy, Ny - 1);
         const double t0 = tb[jx] * cu.xm, t8 = tb[Nvx + jx] * cu.xp;
-        const double t1y = tb[oy + jy] * xym, t7 = tb[oy + Nvy + jy] * xyp;
         const double d2 = tb[ovx + kx], d6 = tb[ovx + g.X + kx], d3 = tb[ovy + ky], d5 = tb[ovy + Ny + ky];
         const double t2v = d2 * xvm, t6 = d6 * xvp, t3 = d3 * xwm, t5 = d5 * xwp, t4 = cu.d * x0;
-        int cm, cp;
-        xcols(rc, cm, cp);
-        const int64_t km = g4_key(cm, 0, n, g), kp = g4_key(cp, 8, n, g);   // stored-order positions
         double s = 0.0;
-        auto add2 = [&](bool pa, int64_t ca, double ta, bool pb, int64_t cb, double tb2) {
-            const bool sw = pa && pb && cb < ca;
-            const double u1 = sw ? tb2 : ta, u2 = sw ? ta : tb2;
-            const bool p1 = sw ? pb : pa, p2 = sw ? pa : pb;
-            s = p1 ? s + u1 : s;
-            s = p2 ? s + u2 : s;
-        };
-        add2(km < rc, km, t0, kp < rc, kp, t8);
-        add2(cym < rc, cym, t1y, cyp < rc, cyp, t7);
-        s = pvm ? s + t2v : s;
-        s = pym ? s + t3 : s;
-        s = s + t4;
-        s = pyp ? s + t5 : s;
-        s = pvp ? s + t6 : s;
-        add2(cym > rc, cym, t1y, cyp > rc, cyp, t7);
-        add2(km > rc, km, t0, kp > rc, kp, t8);
+        // a wave whose rows all sit inside the slab's x range and the y range (no periodic wrap, no
+        // halo plane): the stored order is x-1, y-1, vx-1, vy-1, diag, vy+1, vx+1, y+1, x+1 -- the
+        // general form's select chains below reduce to it term for term (the same adds in the same
+        // order), without the column keys (C4: the waves off a y-line's or a slab's edge, ~95 %)
+        const bool inner = act && rc >= S4 && rc < n - S4 && iy > 0 && iy < Ny - 1;
+        if (fast && __builtin_amdgcn_ballot_w64(!inner) == 0) {
+            const double t1y = tb[oy + jy] * ring[slotm(S3)], t7 = tb[oy + Nvy + jy] * ring[slotp(S3)];
+            s = s + t0;
+            s = s + t1y;
+            s = pvm ? s + t2v : s;
+            s = pym ? s + t3 : s;
+            s = s + t4;
+            s = pyp ? s + t5 : s;
+            s = pvp ? s + t6 : s;
+            s = s + t7;
+            s = s + t8;
+        } else {
+            // in-plane neighbours from the ring (y wraps from the queue)
+            const int cym = iy == 0 ? rc + (Ny - 1) * S3 : rc - S3;
+            const int cyp = iy == Ny - 1 ? rc - (Ny - 1) * S3 : rc + S3;
+            const double xym = iy == 0 ? cu.xw : ring[slotm(S3)];
+            const double xyp = iy == Ny - 1 ? cu.xw : ring[slotp(S3)];
+            const double t1y = tb[oy + jy] * xym, t7 = tb[oy + Nvy + jy] * xyp;
+            int cm, cp;
+            xcols(rc, cm, cp);
+            const int64_t km = g4_key(cm, 0, n, g), kp = g4_key(cp, 8, n, g);   // stored-order positions
+            auto add2 = [&](bool pa, int64_t ca, double ta, bool pb, int64_t cb, double tb2) {
+                const bool sw = pa && pb && cb < ca;
+                const double u1 = sw ? tb2 : ta, u2 = sw ? ta : tb2;
+                const bool p1 = sw ? pb : pa, p2 = sw ? pa : pb;
+                s = p1 ? s + u1 : s;
+                s = p2 ? s + u2 : s;
+            };
+            add2(km < rc, km, t0, kp < rc, kp, t8);
+            add2(cym < rc, cym, t1y, cyp < rc, cyp, t7);
+            s = pvm ? s + t2v : s;
+            s = pym ? s + t3 : s;
+            s = s + t4;
+            s = pyp ? s + t5 : s;
+            s = pvp ? s + t6 : s;
+            add2(cym > rc, cym, t1y, cyp > rc, cyp, t7);
+            add2(km > rc, km, t0, kp > rc, kp, t8);
+        }
         const double sub = (pym && ii > 0) ? 0.0 + d3 : 0.0, sup = (pyp && ii < 7) ? 0.0 + d5 : 0.0;
         double sv = s;
         if constexpr (RES) {   // r = b - A x (iterative.py:816)
@@ -1000,8 +1029,13 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
         }
         // slide the window: the rows of group gi + 1's upper edge (their slots held rows the
         // remaining groups no longer read; the ring is > 2 S3 + 512 long)
-        if (r + GR + S3 < n) ring[slot(GR + S3)] = cu.xn;
-        sb = slot(GR);
+        if (r + GR + S3 < n) {
+            const int t = slotp(GR + S3);
+            ring[t] = cu.xn;
+            if (t < G4RM) ring[RL + t] = cu.xn;
+            if (t >= RL - G4RM) ring[t - RL] = cu.xn;
+        }
+        sb = slotp(GR);
         __syncthreads();
     }
     if constexpr (MODE >= 2) {
@@ -1026,7 +1060,7 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
 
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
                           int fp32, int wgs, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
-                          int col, hipStream_t s, int g_lo, int g_hi, int per_in) {
+                          int col, hipStream_t s, int g_lo, int g_hi, int per_in, int fast) {
     // gr: rows per group = lanes per workgroup (256 or 512)
     const int mode = dots ? dots->mode : 0;
     const int G = g4_ring_group(gr);
@@ -1054,7 +1088,7 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
     const G4Dots dd = dots ? *dots : G4Dots{};
 #define VTK_G4R(VT_, H_, RL_, M_, GR_) \
     hipLaunchKernelGGL((k_g4_ring<VT_, H_, RL_, M_, GR_>), grid, blk, 0, s, g, x, halo, mtri, w, (int)n, (int)per, g_lo, \
-                       g_hi, dd, stop_col, col)
+                       g_hi, dd, stop_col, col, fast)
 #define VTK_G4R_M(VT_, H_, RL_, GR_) \
     do { \
         if (mode == 2) VTK_G4R(VT_, H_, RL_, 2, GR_); \

@@ -140,10 +140,12 @@ inline size_t grid4_tab_len(const Grid4 &g) { return 2 * ((size_t)g.Nvx + g.Nvy 
 // gr >= 512 outside the fused-dots mode 1, else 256).  The solver takes the ring step only for grids
 // that fit (else the SELL grid-row kernels); launch_g4_ring refuses the others
 constexpr int G4TAB = 1024;
+constexpr int G4RM = 64;   // k_g4_ring: mirrored slots at each end of the x ring (> Nvy)
 inline int g4_ring_group(int gr) { return gr >= 512 ? 512 : 256; }
 inline bool g4_ring_fits(const Grid4 &g, int64_t n, int gr) {
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy;
-    return n > 0 && n <= INT32_MAX / 2 && 2 * S3 + 2 * g4_ring_group(gr) <= 8192 && grid4_tab_len(g) <= (size_t)G4TAB;
+    return n > 0 && n <= INT32_MAX / 2 && 2 * S3 + 2 * g4_ring_group(gr) <= 8192 && grid4_tab_len(g) <= (size_t)G4TAB &&
+           g.Nvy < G4RM;
 }
 
 // Tuning switches of a context (vtk_ctx_set_tuning): the defaults are the
@@ -169,6 +171,7 @@ struct Tuning {
                               // (k_g4_ring, ~that many workgroups), step 0's dots and the cycle-start
                               // residual in it too; takes precedence over c4_fused
     int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
+    int g4_fast = 1;          // (A/B) k_g4_ring's straight-line sum for waves of inner rows
     int cyc_ring = 512;       // > 0: cycle-start residual and DCGS2 step 0 through the x-line ring
                               // (k_lsv_ring_epi, ~that many workgroups; 2D line-separable rows)
 };
@@ -520,7 +523,7 @@ struct G4Dots {
 // g_lo, g_hi: the group range (GR-row groups; -1: all), per: groups per workgroup (0: from wgs)
 hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, const double *mtri, double *w, int64_t n,
                           int fp32, int wgs, int gr, const G4Dots *dots, int *grid_out, const int *stop_col,
-                          int col, hipStream_t s, int g_lo = 0, int g_hi = -1, int per = 0);
+                          int col, hipStream_t s, int g_lo = 0, int g_hi = -1, int per = 0, int fast = 1);
 hipError_t launch_band_check(const int32_t *indptr, const int32_t *indices, int64_t n, int L, int X, int *bad,
                              hipStream_t s);
 
