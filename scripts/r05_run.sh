@@ -20,5 +20,18 @@ slabs) for cp in C3:8 C3:4 C3:2 C4:8; do c=${cp%%:*}; p=${cp##*:}
 c4) run bench_c4 600 python bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline ;;
 pmcab) for v in ${AB_VALUES//,/ }; do k=0; for ctr in ${PMC_SETS:-FETCH_SIZE TCC_HIT_sum,TCC_MISS_sum}; do k=$((k+1))
          run pmc_${AB_ENV}_${v}_$k 300 rocprofv3 --pmc ${ctr//,/ } -d gpurun_out/pmc_${AB_ENV}_${v}_$k -o run --output-format csv -- python tools/ab_env.py --env "$AB_ENV" --values "$v" --rounds 1 --config "${AB_CFG:-C3}" --set "${AB_SET:-}"; done; done ;;
+final3) P="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5"
+        run bench_c3 600 python bench.py
+        run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- $P
+        run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- $P
+        run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- $P
+        run bench_upload 600 python bench.py --operator upload --steps 3 --warmup 1 --no-cpu-baseline ;;
+final4) P="python bench.py --config C4 --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5"
+        run bench_c4 600 python bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline
+        run prof_c4 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- $P
+        run pmcf_c4 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_c4 -o run --output-format csv -- $P
+        run pmcw_c4 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_c4 -o run --output-format csv -- $P ;;
+line) run bench_line 300 python bench.py --prec line --steps 5 --warmup 1 --no-cpu-baseline
+      run prof_line 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_line -o run --output-format csv -- python bench.py --prec line --steps 3 --warmup 1 --no-cpu-baseline ;;
 *) echo "unknown stage $st"; exit 2 ;;
 esac; done

@@ -908,7 +908,18 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
             cp = rc < n - S4 ? rc + S4 : (1 - lb) * S4 + rc + S4;
         }
     };
-    auto xat = [&](int c) { return HALO ? *(c >= n ? halo + (c - n) : x + c) : x[c]; };
+    // element i of a kernel-argument array through a 32-bit byte offset (i < 2^28): the load
+    // takes the array base in SGPRs and the offset in one VGPR (no 64-bit address per lane)
+    auto at = [](const auto *base, int i) {
+        using T = std::remove_cv_t<std::remove_pointer_t<decltype(base)>>;
+        return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)i * (uint32_t)sizeof(T));
+    };
+    auto atn = [](const auto *base, int i) {   // (non-temporal: the streamed operands)
+        using T = std::remove_cv_t<std::remove_pointer_t<decltype(base)>>;
+        return __builtin_nontemporal_load(
+            reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)i * (uint32_t)sizeof(T)));
+    };
+    auto xat = [&](int c) { return HALO ? *(c >= n ? halo + (c - n) : x + c) : at(x, c); };
     struct Ld {
         double xn, xm, xp, xw, m, d, b;
         Co c;
@@ -926,16 +937,16 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
     auto load = [&](int gl, Ld &o) {
         const int r = gl * GR + tid;
         const int rc = min(r, n - 1);
-        o.xn = x[min(r + GR + S3, n - 1)];
+        o.xn = at(x, min(r + GR + S3, n - 1));
         int cm, cp;
         xcols(rc, cm, cp);
         o.xm = xat(cm);
         o.xp = xat(cp);
         const int cw = lead.iy == 0 ? rc + (Ny - 1) * S3 : (lead.iy == Ny - 1 ? rc - (Ny - 1) * S3 : rc);
-        o.xw = x[min(max(cw, 0), n - 1)];
-        o.m = __builtin_nontemporal_load(mtri + rc);
-        o.d = (double)__builtin_nontemporal_load(static_cast<const VT *>(g.D) + rc);
-        o.b = RES ? __builtin_nontemporal_load(dd.b + rc) : 0.0;
+        o.xw = at(x, min(max(cw, 0), n - 1));
+        o.m = atn(mtri, rc);
+        o.d = (double)atn(static_cast<const VT *>(g.D), rc);
+        o.b = RES ? atn(dd.b, rc) : 0.0;
         o.c = lead;
         adv(lead);
     };
@@ -1017,7 +1028,7 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
             e0 += sv * sv;
         }
         const double z = bj_trim_group<8>(act ? sv : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
-        if (act) __builtin_nontemporal_store(z, w + r);
+        if (act) __builtin_nontemporal_store(z, reinterpret_cast<double *>(reinterpret_cast<char *>(w) + (uint32_t)r * 8u));
         if constexpr (RES) {
             if (act) e1 += z * z;
         } else if constexpr (MODE == 2) {
