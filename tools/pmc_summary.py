@@ -30,12 +30,12 @@ import statistics
 CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv3 output (default
               # path: SELL-64 layout, tridiagonal-factor BJ(8), DCGS2; fp64 or fp32 values)
     "band_step": r"void vtk::k_band_step<",
-    # k_g4_ring<VT, HALO, RL, PD, MODE, GR>: MODE 0 split step, 1 / 2 with the step's dots, 3 the
+    # k_g4_ring<VT, HALO, RL, MODE, GR>: MODE 0 split step, 2 with step 0's dots, 3 the
     # cycle-start residual; k_lsv_ring_epi<EPI>: 3 residual + BJ, 4 step 0 with its dots
-    "spmv_bj_dc": r"void vtk::k_(sell<(double|float), false, 4, 8, true,|g4_ring<(double|float), (false|true), \d+, \d+, [12], \d+>|lsv_ring_epi<4>)",
+    "spmv_bj_dc": r"void vtk::k_(sell<(double|float), false, 4, 8, true,|g4_ring<(double|float), (false|true), \d+, 2, \d+>|lsv_ring_epi<4>)",
     "spmv": r"void vtk::k_sell<(double|float), false, 0, 1, false,",
-    "spmv_bj": r"void vtk::k_(sell<(double|float), false, 2, 8, true,|g4_ring<(double|float), (false|true), \d+, \d+, 0, \d+>)",
-    "spmv_resid_bj": r"void vtk::k_(sell<(double|float), false, 3, 8, true,|g4_ring<(double|float), (false|true), \d+, \d+, 3, \d+>|lsv_ring_epi<3>)",
+    "spmv_bj": r"void vtk::k_(sell<(double|float), false, 2, 8, true,|g4_ring<(double|float), (false|true), \d+, 0, \d+>)",
+    "spmv_resid_bj": r"void vtk::k_(sell<(double|float), false, 3, 8, true,|g4_ring<(double|float), (false|true), \d+, 3, \d+>|lsv_ring_epi<3>)",
     "spmv_csr": r"void vtk::k_spmv<(double|float), false, 0, 1",
     "spmv_bj_dc_csr": r"void vtk::k_spmv<(double|float), false, 4, 8",
     "dc_dots": r"void vtk::k_dc_dots(_rows<\d+>)?\(",
