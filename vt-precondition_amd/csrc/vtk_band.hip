@@ -1022,22 +1022,29 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
             add2(km > rc, km, t0, kp > rc, kp, t8);
         }
         const double sub = (pym && ii > 0) ? 0.0 + d3 : 0.0, sup = (pyp && ii < 7) ? 0.0 + d5 : 0.0;
-        double sv = s;
-        if constexpr (RES) {   // r = b - A x (iterative.py:816)
-            sv = act ? cu.b - s : 0.0;
-            e0 += sv * sv;
-        }
-        const double z = bj_trim_group<8>(act ? sv : 0.0, lane, act ? sub : 0.0, act ? sup : 0.0, act ? cu.m : 1.0);
-        if (act) __builtin_nontemporal_store(z, reinterpret_cast<double *>(reinterpret_cast<char *>(w) + (uint32_t)r * 8u));
-        if constexpr (RES) {
-            if (act) e1 += z * z;
-        } else if constexpr (MODE == 2) {
-            if (act) {
-                e0 += x0 * x0;
-                e1 += x0 * z;
-                e2 += z * z;
+        // BJ, store and sums; ALL: every lane of the wave holds a row (all but the last group's
+        // waves), so no lane needs the inactive-lane selects
+        auto epi = [&](const bool all) {
+            const bool on = all || act;
+            double sv = s;
+            if constexpr (RES) {   // r = b - A x (iterative.py:816)
+                sv = on ? cu.b - s : 0.0;
+                e0 += sv * sv;
             }
-        }
+            const double z = bj_trim_group<8>(on ? sv : 0.0, lane, on ? sub : 0.0, on ? sup : 0.0, on ? cu.m : 1.0);
+            if (on) __builtin_nontemporal_store(z, reinterpret_cast<double *>(reinterpret_cast<char *>(w) + (uint32_t)r * 8u));
+            if constexpr (RES) {
+                if (on) e1 += z * z;
+            } else if constexpr (MODE == 2) {
+                if (on) {
+                    e0 += x0 * x0;
+                    e1 += x0 * z;
+                    e2 += z * z;
+                }
+            }
+        };
+        if (__builtin_amdgcn_ballot_w64(!act) == 0) epi(true);
+        else epi(false);
         // slide the window: the rows of group gi + 1's upper edge (their slots held rows the
         // remaining groups no longer read; the ring is > 2 S3 + 512 long)
         if (r + GR + S3 < n) {
