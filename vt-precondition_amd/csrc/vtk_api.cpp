@@ -1303,7 +1303,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 int64_t gi_lo = (S4 + G - 1) / G, gi_hi = (n - S4) / G;
                 if (gi_hi <= gi_lo) gi_lo = gi_hi = 0;   // no interior group: all after the exchange
                 const int64_t wgs = std::max(1, c->tune.g4_ring);
-                const int per = (int)std::max<int64_t>({1, (ng + wgs - 1) / wgs, mode ? (ng + GMAX - 4) / (GMAX - 3) : 1});
+                const int per = (int)std::max<int64_t>({g4_ring_per(ng, S4, G, (int)wgs), mode ? (ng + GMAX - 4) / (GMAX - 3) : 1});
                 const bool exch = s.A->n_send > 0 || s.A->n_halo > 0 || c->host_comm;
                 if (exch) TRY(halo_exchange_async(s.A, pj));
                 int gin = 0, gb0 = 0, gb1 = 0;

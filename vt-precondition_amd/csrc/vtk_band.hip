@@ -1088,7 +1088,7 @@ hipError_t launch_g4_ring(const Grid4 &g, const double *x, const double *halo, c
     // the ring: the window 2 S3 + G plus the next group's rows
     const bool small = 2 * S3 + 2 * G <= (G == 256 ? 4608 : 5120);
     const int64_t ng = (n + G - 1) / G;
-    int64_t per = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
+    int64_t per = g4_ring_per(ng, S4, G, wgs);
     // the fused reductions write one partial per workgroup: at most GMAX workgroups
     if (mode) per = std::max<int64_t>(per, (ng + GMAX - 1) / GMAX);
     // a group range [g_lo, g_hi) of the launch (the interior / boundary planes of a rank's slab

@@ -1,6 +1,7 @@
 // vtk_internal.hpp — types shared by the C-ABI/driver (vtk_api.cpp, vtk_host.cpp) and the
 // gfx950 kernels (vtk_kernels.hip).  Not part of the public ABI.
 #pragma once
+#include <cmath>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
@@ -142,6 +143,20 @@ inline size_t grid4_tab_len(const Grid4 &g) { return 2 * ((size_t)g.Nvx + g.Nvy 
 constexpr int G4TAB = 1024;
 constexpr int G4RM = 64;   // k_g4_ring: mirrored slots at each end of the x ring (> Nvy)
 inline int g4_ring_group(int gr) { return gr >= 512 ? 512 : 256; }
+// groups per workgroup of a k_g4_ring launch over ng groups of G rows for ~wgs workgroups,
+// XCD-aligned: a workgroup's x -+ 1 plane rows belong to the workgroups q = S4 / (per G) indices
+// away; per is rounded so that q is a multiple of 8, which puts them on the same XCD (workgroups
+// are dealt round-robin over the eight XCDs) -- those reads hit its L2 (C4: per 48 -> 31, ring
+// 384 -> 369 us)
+// (only where a plane spans >= 8 groups and q would stay <= 32: with a few groups per
+// workgroup the rounding cannot hold q near a multiple of 8)
+inline int64_t g4_ring_per(int64_t ng, int64_t S4, int G, int wgs) {
+    const int64_t per0 = std::max<int64_t>(1, (ng + std::max(1, wgs) - 1) / std::max(1, wgs));
+    const double gpp = (double)S4 / G;   // groups per x-plane
+    if (gpp < 8.0 || gpp / (double)per0 > 32.0) return per0;
+    const int64_t q = std::max<int64_t>(8, (int64_t)std::ceil(gpp / (double)per0 / 8.0) * 8);
+    return std::max<int64_t>(1, std::llround(gpp / (double)q));
+}
 inline bool g4_ring_fits(const Grid4 &g, int64_t n, int gr) {
     const int64_t S3 = (int64_t)g.Nvx * g.Nvy;
     return n > 0 && n <= INT32_MAX / 2 && 2 * S3 + 2 * g4_ring_group(gr) <= 8192 && grid4_tab_len(g) <= (size_t)G4TAB &&
