@@ -31,6 +31,7 @@ final4) P="python bench.py --config C4 --steps 1 --warmup 1 --no-cpu-baseline --
         run prof_c4 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- $P
         run pmcf_c4 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_c4 -o run --output-format csv -- $P
         run pmcw_c4 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_c4 -o run --output-format csv -- $P ;;
+sq) run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py ${SQ_ARGS:-} --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
 line) run bench_line 300 python bench.py --prec line --steps 5 --warmup 1 --no-cpu-baseline
       run prof_line 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_line -o run --output-format csv -- python bench.py --prec line --steps 3 --warmup 1 --no-cpu-baseline ;;
 *) echo "unknown stage $st"; exit 2 ;;
