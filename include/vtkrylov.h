@@ -170,7 +170,7 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
  * with and without a byte-saving form).  Each key is seeded from the environment variable
  * VTK_<KEY in upper case> once, when the context is created; the library reads its environment
  * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_opt, lsv_ring, prof_perj,
- * comm_solo, auto_band, grid4, c4_fused, g4_ring, g4_gr, g4_fast, cyc_ring.
+ * comm_solo, auto_band, grid4, c4_fused, g4_ring, g4_gr, g4_fast, line_fuse, cyc_ring.
  * VTK_ERR_ARG for an unknown key; a VTK_<KEY> variable of a key removed in round 5 draws a
  * warning on stderr at context creation and is otherwise ignored.  (ABI 5) */
 int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);

@@ -243,9 +243,10 @@ def test_line_ranks_sharing_one_gpu(tmp_path, case, world, orth):
 
 
 @pytest.mark.parametrize("name", SMALL + ["C1"])
-def test_compact_apply_bitexact_vs_stored_factors(ops, vk_lib, name):
+def test_compact_apply_bitexact_vs_stored_factors(ops, gpu, vk_lib, name):
     """The Vlasov operators' x-couplings are constant along each line: the compact apply (l, g
-    formed from a_j, c_j and m) must give the stored-factor apply's bits, in GMRES too."""
+    formed from a_j, c_j and m) must give the stored-factor apply's bits, in GMRES too (both
+    through the two-kernel line step, line_fuse 0: the fused one needs the compact factors)."""
     vk = vk_lib
     p, A, _ = ops[name]
     M = vk.line_jacobi(A, stride_of(p), SEG)
@@ -253,11 +254,13 @@ def test_compact_apply_bitexact_vs_stored_factors(ops, vk_lib, name):
     r = twin.rhs(p.n)
     zc = M @ r
     b = twin.rhs(p.n)
-    xc, ic = vk.gmres(A, b, rtol=1e-8, M=M)
+    with gpu.tuning(line_fuse=0):
+        xc, ic = vk.gmres(A, b, rtol=1e-8, M=M)
     M.set_compact(False)
     assert not M.compact
     assert np.array_equal(bits(zc), bits(M @ r))
-    xg, ig = vk.gmres(A, b, rtol=1e-8, M=M)
+    with gpu.tuning(line_fuse=0):
+        xg, ig = vk.gmres(A, b, rtol=1e-8, M=M)
     assert ic == ig == 0 and np.array_equal(bits(xc), bits(xg))
 
 
@@ -309,20 +312,54 @@ def test_line_path_separable_spmv_bit_identical(vk_lib, gpu):
     assert A.line_separable
     M = vk_lib.line_jacobi(A, vk_lib.vlasov_line_stride(vk_lib.vlasov_params(p.dim, p.shape)), 25)
     b = twin.rhs(p.n)
-    x1, i1 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
-    it1 = vk_lib.last_stats().inner_iters
-    with gpu.tuning(band_lsv=0):
+    # (line_fuse 0: the SpMV as its own kernel, whose output the sweep kernel reads)
+    with gpu.tuning(line_fuse=0):
+        x1, i1 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
+        it1 = vk_lib.last_stats().inner_iters
+    with gpu.tuning(band_lsv=0, line_fuse=0):
         x0, i0 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
     assert i1 == i0 == 0 and it1 == vk_lib.last_stats().inner_iters
     assert np.array_equal(x1, x0)
-    with gpu.tuning(sell_canon=0):   # the SELL codes instead of canon_row's columns
+    with gpu.tuning(sell_canon=0, line_fuse=0):   # the SELL codes instead of canon_row's columns
         x2, i2 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
     assert i2 == 0 and it1 == vk_lib.last_stats().inner_iters
     assert np.array_equal(x1, x2)
     for wgs in (64, 2048):   # x staged through LDS (k_lsv_ring): the same products, the same order
-        with gpu.tuning(lsv_ring=wgs):
+        with gpu.tuning(lsv_ring=wgs, line_fuse=0):
             x3, i3 = vk_lib.gmres(A, b, rtol=1e-8, M=M)
         assert i3 == 0 and it1 == vk_lib.last_stats().inner_iters
         assert np.array_equal(x1, x3), wgs
+    M.close()
+    A.close()
+
+
+@pytest.mark.parametrize("name,seg", [("C1", 25), ("S2", 8), ("S2", 3), ("C1", 32)])
+def test_line_spmv_fused_into_sweep(vk_lib, gpu, name, seg):
+    """The default one-rank line path forms the SpMV inside the sweep kernel (k_line_spmv_dc,
+    DESIGN.md §3f): the same products, order and sweeps, the dots grouped by 62-lane blocks --
+    within the DCGS2 bars of the two-kernel form, deterministic, and against the C oracle's
+    line-Jacobi GMRES; x0 != 0 and restart 5 (several cycles) too."""
+    import numpy as np
+    from oracle import twin
+    p = twin.CONFIGS[name]
+    A = vk_lib.vlasov_operator(vk_lib.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=gpu)
+    M = vk_lib.line_jacobi(A, vk_lib.vlasov_line_stride(vk_lib.vlasov_params(p.dim, p.shape)), seg)
+    b = twin.rhs(p.n)
+    x0 = twin.rhs(p.n, seed=0xB0B) * 1e-3
+    for kw in ({}, {"x0": x0}, {"restart": 5}):
+        gpu.profile(True)
+        xf, i_f = vk_lib.gmres(A, b, rtol=1e-8, M=M, orth="dcgs2", **kw)
+        st_f = vk_lib.last_stats()
+        prof = gpu.profile_read()
+        gpu.profile(False)
+        assert "spmv_lsv" not in prof or prof["spmv_lsv"]["launches"] == 0, sorted(prof)   # the fused kernel ran
+        xg, _ = vk_lib.gmres(A, b, rtol=1e-8, M=M, orth="dcgs2", **kw)
+        assert np.array_equal(xf, xg) and vk_lib.last_stats().inner_iters == st_f.inner_iters
+        with gpu.tuning(line_fuse=0):
+            xu, i_u = vk_lib.gmres(A, b, rtol=1e-8, M=M, orth="dcgs2", **kw)
+            st_u = vk_lib.last_stats()
+        assert i_f == i_u == 0, kw
+        assert abs(st_f.inner_iters - st_u.inner_iters) <= 1, kw
+        assert np.linalg.norm(xf - xu) / np.linalg.norm(xu) < 1e-9, kw
     M.close()
     A.close()

@@ -81,7 +81,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"band_canon", &Tuning::band_canon}, {"band_opt", &Tuning::band_opt}, {"lsv_ring", &Tuning::lsv_ring},
     {"prof_perj", &Tuning::prof_perj}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring},
-    {"g4_gr", &Tuning::g4_gr}, {"g4_fast", &Tuning::g4_fast}, {"cyc_ring", &Tuning::cyc_ring},
+    {"g4_gr", &Tuning::g4_gr}, {"g4_fast", &Tuning::g4_fast}, {"line_fuse", &Tuning::line_fuse}, {"cyc_ring", &Tuning::cyc_ring},
 };
 // switches of earlier rounds whose alternative lost its A/B: an environment that
 // still sets one is told once that it no longer has an effect
@@ -1259,7 +1259,15 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         } else if (line_dc) {
             // line path: SpMV, then the line sweeps with the step's dots fused behind them
             TRY(halo_exchange(s.A, pj));
-            if (line_lsv) {
+            const LineOp &lo = s.M->line;
+            if (line_canon && c->tune.line_fuse && !c->dist && lo.compact && lo.stride == s.A->band_L &&
+                lo.row0 == 0 && lo.n == n && lo.j0 == 0 && lo.jn == lo.stride && lo.ac && lo.i_lo == 0 &&
+                lo.i_hi == n / lo.stride - 1 && n / lo.stride >= 3 && lo.seg <= 32) {
+                // one rank: the SpMV inside the sweep kernel (y never stored)
+                Prof pf(c, "line_dc", j, b_inv + 8.0 * (double)n + n8 * (j + 2));   // m, D, p, w, V_j
+                HIPCHK(c, launch_line_spmv_dc(lo, s.A->d_lsv, pj, s.w, s.V, s.ld, j, s.dcpart, s.G, stop, j, c->stream));
+                cnt = s.G;
+            } else if (line_lsv) {
                 // line-separable values: 12 B of matrix per row (codes + diagonal)
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
                 HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
@@ -1271,9 +1279,11 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
                                       nullptr, stop, j, c->stream));
             }
-            { Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
-              HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream)); }
-            cnt = s.G;
+            if (!cnt) {
+                Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
+                HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream));
+                cnt = s.G;
+            }
         } else if (ring4) {
             // step 0's dots (|p|^2, p.w, |w|^2) in the same sweep; the later steps' dots in
             // k_dc_dots (fused into the ring they cost 215.6 vs 201.5 ms per C4 solve: the ring

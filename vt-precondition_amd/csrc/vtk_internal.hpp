@@ -187,6 +187,7 @@ struct Tuning {
                               // residual in it too; takes precedence over c4_fused
     int g4_gr = 512;          // k_g4_ring: rows per group = lanes per workgroup (256 | 512)
     int g4_fast = 1;          // (A/B) k_g4_ring's straight-line sum for waves of inner rows
+    int line_fuse = 1;        // line path (one rank, canonical rows): the SpMV inside the sweep kernel
     int cyc_ring = 512;       // > 0: cycle-start residual and DCGS2 step 0 through the x-line ring
                               // (k_lsv_ring_epi, ~that many workgroups; 2D line-separable rows)
 };
@@ -375,6 +376,10 @@ hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, cons
 // launch_dc_dots layout); hipErrorInvalidValue when the segments are too long (> 32)
 hipError_t launch_line_dc(const LineOp &L, const double *r, double *w, const double *V, int64_t ld, int j,
                           const double *p, double *part, int grid, const int *stop_col, int col, hipStream_t s);
+// the same with y = A p formed inside (k_line_spmv_dc): one rank, canonical line-separable rows
+// (lsv: vtk_csr::d_lsv), lines of L.stride rows, compact factors; hipErrorInvalidValue otherwise
+hipError_t launch_line_spmv_dc(const LineOp &L, const double *lsv, const double *p, double *w, const double *V,
+                               int64_t ld, int j, double *part, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_line_apply(const LineOp &L, const double *r, double *z, const double *v0, double *part0,
                              double *part1, int grid, const int *stop_col, int col, hipStream_t s);
 hipError_t launch_bj_tri_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,

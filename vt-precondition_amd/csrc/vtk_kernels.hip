@@ -1546,6 +1546,171 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
     }
 }
 
+// Line path, one rank, canonical line-separable rows: the table SpMV y = A p
+// formed inside the sweep kernel -- the lane's column of p along its segment, one line either
+// side, in registers; p at v -+ 1 from the neighbouring lanes (a wave covers 62 positions plus
+// one halo column each side) -- then k_line_apply's sweeps and dots on it (COMPACT, DCD).  y is
+// neither written nor read back (two vectors less per step) and p is read once for the SpMV and
+// the dots.  The SpMV's products and their order are k_lsv_ring's (canonical row order), the
+// sweeps k_line_apply's: w is bit-identical to the two-kernel form; the dots' partials follow the
+// 62-lane blocks (another fixed order: the DCGS2 bars).
+template <int LMAX>
+__global__ __launch_bounds__(NT) void k_line_spmv_dc(LineOp L, const double *__restrict__ lsv,
+                                                     const double *__restrict__ p, double *__restrict__ w, int nb,
+                                                     const int *stop_col, int col, LineDc dc) {
+    constexpr int NQW = 2 * DC_MAXJ + 3;
+    __shared__ double stage[(NT / 64) * NQW];
+    if (stopped(stop_col, col)) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = (int)L.n, Lb = (int)L.stride, X = n / Lb, seg = (int)L.seg;
+    const int64_t nitems = L.nseg * nb;
+    const double *m = L.f + L.n;
+    double dsl = 0.0, dzl = 0.0, daa = 0.0, dab = 0.0, dag = 0.0;
+    for (int64_t t = (int64_t)blockIdx.x * (NT / 64) + wv; t < nitems; t += (int64_t)gridDim.x * (NT / 64)) {
+        const int sg = (int)(t / nb), jw = (int)(t - (int64_t)sg * nb);
+        const int xb = sg * seg, len = min(seg, X - xb);
+        const int vv = jw * 62 + lane - 1;   // lanes 0 and 63: the halo columns v - 1, v + 1
+        const bool inl = vv >= 0 && vv < Lb;
+        const bool use = inl && lane >= 1 && lane <= 62;
+        const int v = inl ? vv : 0;
+        const double aj = use ? L.ac[v] : 0.0, cj = use ? L.ac[L.jn + v] : 0.0;
+        const double tx0 = lsv[n + v], tx1 = lsv[n + Lb + v];
+        // p on the column: lines xb - 1 .. xb + len (periodic in x)
+        double pc[LMAX + 2];
+#pragma unroll
+        for (int u = 0; u < LMAX + 2; ++u) {
+            int x = xb - 1 + min(u, len + 1);
+            x = x < 0 ? x + X : (x >= X ? x - X : x);
+            pc[u] = ld_nt<8>(p + (x * Lb + v));
+        }
+        double e[LMAX], gg[LMAX];
+        double dp = 0.0, mp = 0.0;
+        bool pok = false;
+        unsigned okm = 0;
+#pragma unroll
+        for (int u = 0; u < LMAX; ++u) {
+            const bool ok = use && u < len;
+            const int x = xb + min(u, len - 1);
+            const int k = ok ? x * Lb + v : 0;
+            const double mv = ld_nt<8>(m + k);
+            // y(x, v): the row's five terms in the canonical order of line x (k_lsv_ring)
+            const double drow = ld_nt<8>(lsv + (x * Lb + v));
+            const double tv0 = lsv[n + 2 * Lb + x], tv1 = lsv[n + 2 * Lb + X + x];
+            const double c0 = pc[u + 1];
+            const double pm = __shfl_up(c0, 1, 64), pq = __shfl_down(c0, 1, 64);
+            const double t0 = tx0 * pc[u], t4 = tx1 * pc[u + 2], t2 = drow * c0, t1 = tv0 * pm, t3 = tv1 * pq;
+            const bool h1 = v > 0, h3 = v < Lb - 1;
+            double sa = 0.0;
+            if (x == 0) {   // x - 1 wraps to line X - 1: last
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+                sa = sa + t4;
+                sa = sa + t0;
+            } else if (x == X - 1) {   // x + 1 wraps to line 0: first
+                sa = sa + t4;
+                sa = sa + t0;
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+            } else {
+                sa = sa + t0;
+                sa = h1 ? sa + t1 : sa;
+                sa = sa + t2;
+                sa = h3 ? sa + t3 : sa;
+                sa = sa + t4;
+            }
+            // k_line_apply<LMAX, COMPACT>'s forward sweep on r = y
+            const bool hl = ok && pok;
+            const bool hr = ok && u + 1 < len && k + Lb < n;
+            const double lv = hl ? aj * mp : 0.0;
+            const double gv = (hr ? cj : 0.0) * mv;
+            const double dv = sa - lv * dp;
+            e[u] = mv * dv;
+            gg[u] = gv;
+            if (ok) {
+                dp = dv;
+                mp = mv;
+            }
+            pok = ok;
+            okm |= (unsigned)ok << u;
+        }
+        double zn = 0.0;
+#pragma unroll
+        for (int u = LMAX - 1; u >= 0; --u) {
+            const double zv = e[u] - gg[u] * zn;
+            if ((okm >> u) & 1u) {
+                st_nt<4>(w + ((xb + u) * Lb + v), zv);
+                zn = zv;
+            }
+            e[u] = ((okm >> u) & 1u) ? zv : 0.0;   // w, kept for the dots
+        }
+        // the dots (k_line_apply's DCD), p from the column
+#pragma unroll
+        for (int u = 0; u < LMAX; ++u) gg[u] = ((okm >> u) & 1u) ? pc[u + 1] : 0.0;
+#pragma unroll
+        for (int u = 0; u < LMAX; ++u) {
+            daa += gg[u] * gg[u];
+            dab += gg[u] * e[u];
+            dag += e[u] * e[u];
+        }
+        for (int kk = 0; kk < dc.j; ++kk) {
+            const double *vk = dc.V + (size_t)kk * dc.ld;
+            double sl = 0.0, zl = 0.0;
+#pragma unroll
+            for (int u = 0; u < LMAX; ++u) {
+                const double vvk = ((okm >> u) & 1u) ? __builtin_nontemporal_load(vk + ((xb + u) * Lb + v)) : 0.0;
+                sl += vvk * gg[u];
+                zl += vvk * e[u];
+            }
+            const double ts = wave_allsum(sl), tz = wave_allsum(zl);
+            if (lane == kk) {
+                dsl += ts;
+                dzl += tz;
+            }
+        }
+    }
+    double *rec = stage + wv * NQW;
+    if (lane < dc.j) {
+        rec[lane] = dsl;
+        rec[DC_MAXJ + lane] = dzl;
+    }
+    const double t0 = wave_sum(daa), t1 = wave_sum(dab), t2 = wave_sum(dag);
+    if (lane == 0) {
+        rec[2 * DC_MAXJ] = t0;
+        rec[2 * DC_MAXJ + 1] = t1;
+        rec[2 * DC_MAXJ + 2] = t2;
+    }
+    __syncthreads();
+    for (int qq = threadIdx.x; qq < DC_NQ; qq += NT) {
+        const bool used = qq < dc.j || (qq >= DC_MAXJ && qq < DC_MAXJ + dc.j) || qq >= 2 * DC_MAXJ;
+        if (used) {
+            double t = 0.0;
+#pragma unroll
+            for (int w2 = 0; w2 < NT / 64; ++w2) t += stage[w2 * NQW + qq];
+            dc.part[(size_t)qq * GMAX + blockIdx.x] = t;
+        }
+    }
+}
+
+hipError_t launch_line_spmv_dc(const LineOp &L, const double *lsv, const double *p, double *w, const double *V,
+                               int64_t ld, int j, double *part, int grid, const int *stop_col, int col, hipStream_t s) {
+    const int64_t Lb = L.stride, X = Lb > 0 ? L.n / Lb : 0;
+    // one rank's whole slab, lines of Lb rows, the lanes over every position, compact factors
+    if (!L.compact || !L.ac || L.row0 != 0 || Lb <= 0 || L.n % Lb != 0 || X < 3 || L.j0 != 0 || L.jn != Lb ||
+        L.i_lo != 0 || L.i_hi != X - 1 || L.seg <= 0 || L.seg > 32 || j < 0 || j > DC_MAXJ || grid < 1 ||
+        grid > GMAX || L.n > INT32_MAX / 2 || !lsv || !p || !part)
+        return hipErrorInvalidValue;
+    const int nb = (int)((Lb + 61) / 62);
+    const dim3 g(grid), b(NT);
+    const LineDc dc{V, ld, j, p, part};
+    if (L.seg <= 8) hipLaunchKernelGGL(k_line_spmv_dc<8>, g, b, 0, s, L, lsv, p, w, nb, stop_col, col, dc);
+    else if (L.seg <= 16) hipLaunchKernelGGL(k_line_spmv_dc<16>, g, b, 0, s, L, lsv, p, w, nb, stop_col, col, dc);
+    else if (L.seg <= 25) hipLaunchKernelGGL(k_line_spmv_dc<25>, g, b, 0, s, L, lsv, p, w, nb, stop_col, col, dc);
+    else hipLaunchKernelGGL(k_line_spmv_dc<32>, g, b, 0, s, L, lsv, p, w, nb, stop_col, col, dc);
+    return hipGetLastError();
+}
+
 hipError_t launch_line_setup(const int32_t *indptr, const int32_t *indices, const void *data, int fp32,
                              const LineOp &L, unsigned long long *bad_row, unsigned long long *ext, hipStream_t s) {
     const int64_t threads = L.nseg * L.jb * 64;
