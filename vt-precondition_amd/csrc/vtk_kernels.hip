@@ -1548,7 +1548,7 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
 
 // Line path, one rank, canonical line-separable rows: the table SpMV y = A p
 // formed inside the sweep kernel -- the lane's column of p along its segment, one line either
-// side, in registers; p at v -+ 1 from the neighbouring lanes (a wave covers 62 positions plus
+// side, in registers; p at v -+ 1 from the neighbouring lanes (DPP wave shifts; a wave covers 62 positions plus
 // one halo column each side) -- then k_line_apply's sweeps and dots on it (COMPACT, DCD).  y is
 // neither written nor read back (two vectors less per step) and p is read once for the SpMV and
 // the dots.  The SpMV's products and their order are k_lsv_ring's (canonical row order), the
@@ -1597,7 +1597,8 @@ __global__ __launch_bounds__(NT) void k_line_spmv_dc(LineOp L, const double *__r
             const double drow = ld_nt<8>(lsv + (x * Lb + v));
             const double tv0 = lsv[n + 2 * Lb + x], tv1 = lsv[n + 2 * Lb + X + x];
             const double c0 = pc[u + 1];
-            const double pm = __shfl_up(c0, 1, 64), pq = __shfl_down(c0, 1, 64);
+            // v -+ 1: the neighbouring lanes' values by DPP wave shifts (wave_shr:1 / wave_shl:1)
+            const double pm = dpp_mov<0x138>(c0), pq = dpp_mov<0x130>(c0);
             const double t0 = tx0 * pc[u], t4 = tx1 * pc[u + 2], t2 = drow * c0, t1 = tv0 * pm, t3 = tv1 * pq;
             const bool h1 = v > 0, h3 = v < Lb - 1;
             double sa = 0.0;
