@@ -210,9 +210,9 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
         vreg[J] = vj;
         if (kind == 0 && own) {
             if (j >= 1) {
-                __builtin_nontemporal_store(vj, a.V + (size_t)j * a.ld + row);
+                st_wt(a.V + (size_t)j * a.ld + row, vj);
             }
-            if (j == a.m - 2) __builtin_nontemporal_store(pn, a.V + (size_t)(j + 1) * a.ld + row);
+            if (j == a.m - 2) st_wt(a.V + (size_t)(j + 1) * a.ld + row, pn);
         }
         return pn;
     };
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             }
             const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
             if (own) {
-                __builtin_nontemporal_store(z, a.w_out + row);
+                st_wt(a.w_out + row, z);
                 wbuf[tid - 8] = z;
             }
             __syncthreads();
@@ -816,7 +816,7 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring(const double *__restrict__ 
                 sa = sa + t2;
                 sa = h3 ? sa + t3 : sa;
             }
-            if (own) __builtin_nontemporal_store(sa, y + (int64_t)xl * L + v);
+            if (own) st_nt<2>(y + (int64_t)xl * L + v, sa);
         }
     }
 }
@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
                 e0 += sv * sv;
             }
             const double z = bj_trim_group<8>(on ? sv : 0.0, lane, on ? sub : 0.0, on ? sup : 0.0, on ? cu.m : 1.0);
-            if (on) __builtin_nontemporal_store(z, reinterpret_cast<double *>(reinterpret_cast<char *>(w) + (uint32_t)r * 8u));
+            if (on) st_nt<2>(reinterpret_cast<double *>(reinterpret_cast<char *>(w) + (uint32_t)r * 8u), z);
             if constexpr (RES) {
                 if (on) e1 += z * z;
             } else if constexpr (MODE == 2) {
@@ -1249,7 +1249,7 @@ __global__ __launch_bounds__(BAND_T) void k_lsv_ring_epi(LsvEpiK a) {
                 }
                 out = z;
             }
-            if (own) __builtin_nontemporal_store(out, a.y + row);
+            if (own) st_nt<2>(a.y + row, out);
         }
     }
     const int wid = tid >> 6;

@@ -217,6 +217,13 @@ __device__ __forceinline__ d2v ldnt2(const double *p) {
 // non-temporal loads of operands read once per kernel (NT_LOADS bits: 1 fused BJ m, +2.5 % on
 // the C3 BJ path; 4 dots p/w and 8 line apply r/m, +1 % on the line path)
 constexpr int NT_STORES = 6, NT_LOADS = 13;
+// write-through (sc1) store of a streamed-out result: the line leaves the XCD's L2 with the store,
+// so the release at the kernel's end finds no dirty lines to write back (plain and nt stores keep
+// them: MI355X_MICROARCH.md, store flavours).  The band step's v_j / w stores: C3/8 slab
+// 9 811 -> 9 971 it/s, C3 +0.5 % (round 5)
+__device__ __forceinline__ void st_wt(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <int BIT>
 __device__ __forceinline__ double ld_nt(const double *p) {
     if constexpr ((NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
@@ -481,7 +488,8 @@ static __device__ __forceinline__ void dc_xupdate_body(const double *__restrict_
             double2 xv = *reinterpret_cast<const double2 *>(x + i);
             xv.x = xv.x + ax;
             xv.y = xv.y + ay;
-            st_nt2<1>(x + i, xv.x, xv.y);
+            st_wt(x + i, xv.x);   // (write-through: C3 x update 652 -> 630 us, C4 1 615 -> 1 558 us)
+            st_wt(x + i + 1, xv.y);
         } else {
             double ax = 0.0, a = c == j ? pj[i] : 0.0;
             if (rec) {

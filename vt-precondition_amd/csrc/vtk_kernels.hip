@@ -2622,13 +2622,13 @@ __global__ __launch_bounds__(NT) void k_dc_update(double *__restrict__ V, int64_
             if (j >= 1) {
                 vj.x = a.x * rinv;
                 vj.y = a.y * rinv;
-                __builtin_nontemporal_store(d2v{vj.x, vj.y}, reinterpret_cast<d2v *>(pj + i));
+                st_nt2<2>(pj + i, vj.x, vj.y);
             }
             t.x = t.x - ej * vj.x;
             t.y = t.y - ej * vj.y;
             t.x = t.x * q;
             t.y = t.y * q;
-            __builtin_nontemporal_store(d2v{t.x, t.y}, reinterpret_cast<d2v *>(pn + i));
+            st_nt2<2>(pn + i, t.x, t.y);
         } else {
             const double p = pj[i];
             double a = p, t = w[i];
