@@ -1203,7 +1203,9 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                                           : b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n)
                                    : b_csr;
     bool broke = false;
-    constexpr int ev_every = 1;   // (every 2 or 4 steps measured neutral)
+    // an event every 4 steps: r05 library A/B (profiles/r05_ev_every_ab.json) C3/8 slab +2 %,
+    // C3 +0.6 %; a stop is acted on at most 3 steps later (early-exit launches, ~us each)
+    constexpr int ev_every = 4;
     int ev_step[LOOKAHEAD + 1];
     int nev = 0, synced = 0;
     for (int j = 0; j < m; ++j) {
@@ -1407,7 +1409,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             Prof pf(c, "dc_update", j, n8 * (j + 4));
             HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1, c->stream));
         }
-        // throttle: an event every EV_EVERY steps (each record costs the stream a few us); the
+        // throttle: an event every ev_every steps (each record costs the stream a few us); the
         // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
         // has passed there.  Column cc stops in step cc (early commit) or cc+1: act only once
         // every rank ran it.
