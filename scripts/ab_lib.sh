@@ -15,6 +15,6 @@ for rep in $(seq 1 "$reps"); do
     python3 -c "
 import json
 d=json.loads([l for l in open('gpurun_out/abl_${v}_$rep.log') if l.startswith('{')][-1])
-print('$v', $rep, round(d['value'],1), {k: round(e['avg_us'],1) for k, e in d['kernels'].items() if k in ('band_step','xupdate','spmv_bj','line_dc','dc_scalar','dc_finalize')})"
+print('$v', $rep, round(d['value'],1), {k: round(e['avg_us'],1) for k, e in d['kernels'].items() if k in ('band_step','xupdate','spmv_bj','line_dc','dc_scalar','dc_finalize','dc_update','dc_dots')})"
   done
 done
