@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTK_ABI_VERSION 5
+#define VTK_ABI_VERSION 6   /* 6: VTK_ERR_PEER, vtk_precond_matvec */
 
 typedef struct vtk_ctx vtk_ctx;
 typedef struct vtk_csr vtk_csr;
@@ -50,7 +50,9 @@ typedef enum {
     VTK_ERR_SINGULAR = -4,  /* singular diagonal block (numpy.linalg.LinAlgError)  */
     VTK_ERR_NOMEM = -5,     /* host or device allocation failed                    */
     VTK_ERR_STATE = -6,     /* call not valid in this state (e.g. comm not set)    */
-    VTK_ERR_NODEVICE = -7   /* no HIP device: the product has no CPU fallback      */
+    VTK_ERR_NODEVICE = -7,  /* no HIP device: the product has no CPU fallback      */
+    VTK_ERR_PEER = -8       /* another rank failed mid-solve; this rank left the   */
+                            /* solve at the same Arnoldi step (vtk_gmres)          */
 } vtk_status;
 
 typedef enum { VTK_PTR_HOST = 0, VTK_PTR_DEVICE = 1 } vtk_ptr_kind;
@@ -169,10 +171,12 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
  * settings exist for in-process A/B measurements and for the bit-identity tests (the same sums
  * with and without a byte-saving form).  Each key is seeded from the environment variable
  * VTK_<KEY in upper case> once, when the context is created; the library reads its environment
- * nowhere else.  Keys: band, band_lsv, sell_canon, band_canon, band_opt, lsv_ring, prof_perj,
- * comm_solo, auto_band, grid4, c4_fused, g4_ring, g4_gr, g4_fast, line_fuse, cyc_ring.
+ * nowhere else (fail_step is a test hook: this rank fails its DCGS2 step of that index in the
+ * first cycle, vtk_gmres).  Keys: band, band_lsv, sell_canon, band_canon, band_opt, lsv_ring,
+ * prof_perj, comm_solo, auto_band, grid4, c4_fused, g4_ring, g4_gr, g4_fast, line_fuse, cyc_ring,
+ * fail_step.
  * VTK_ERR_ARG for an unknown key; a VTK_<KEY> variable of a key removed in round 5 draws a
- * warning on stderr at context creation and is otherwise ignored.  (ABI 5) */
+ * warning on stderr at context creation and is otherwise ignored.  (ABI 5; fail_step ABI 6) */
 int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);
 int vtk_ctx_get_tuning(vtk_ctx *ctx, const char *key, int *value);
 /* rank 0 creates the 128-byte RCCL unique id; the caller broadcasts it (any transport) */
@@ -299,11 +303,25 @@ int vtk_linejacobi_get_compact(vtk_prec *M, int *in_use, int *available);
 /* z = M^-1 r for any preconditioner; *kind = vtk_prec_kind */
 int vtk_prec_apply(vtk_prec *M, const double *r, double *z, int ptr_kind);
 int vtk_prec_kind_of(vtk_prec *M, int *kind);
+/* w = M^-1 (A x): the preconditioned operator GMRES applies at every Arnoldi step (SciPy:
+ * M.matvec(A @ x), iterative.py:752), computed by the launch the solver's split DCGS2 step uses
+ * for this operator and preconditioner (the 4D grid-row ring kernel -- across ranks in the
+ * solver's interior / boundary form --, else the SpMV with the BJ epilogue, else SpMV then
+ * apply); M may be NULL (w = A x).  Bit-identical across those forms: the kernel-level pin. */
+int vtk_precond_matvec(vtk_csr *A, vtk_prec *M, const double *x, double *w, int ptr_kind);
 
 /* ---- solver --------------------------------------------------------------------------- */
 /* scipy.sparse.linalg.gmres semantics (iterative.py:582-841, callback=None): restarted,
  * left-preconditioned GMRES(restart); maxiter counts restart cycles (<= 0: 10 n); x holds
- * x0 on entry and the solution on exit; info = 0 on convergence else maxiter. */
+ * x0 on entry and the solution on exit; info = 0 on convergence else maxiter.
+ * Across ranks (DCGS2): a rank whose launch fails mid-solve returns its error, and every
+ * rank -- the failing one included -- leaves the solve after the same Arnoldi step: the
+ * failure travels as a vote in the step's all-reduce, so no rank is left blocked in a
+ * collective; the peers return VTK_ERR_PEER and the communicator stays usable.  A failed
+ * collective itself (VTK_ERR_RCCL) marks the communicator broken: vtk_ctx_destroy then
+ * aborts it (ncclCommAbort) instead of destroying it.  (The modelled failure is a launch the
+ * rank could not issue; a device fault that kills the HIP context cannot join any collective
+ * and is left to the launcher's watchdog.) */
 int vtk_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, double atol,
               int restart, int64_t maxiter, int ptr_kind, int *info, vtk_stats *stats);
 int vtk_gmres_set_orth(vtk_ctx *ctx, int orth);

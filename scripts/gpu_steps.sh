@@ -35,7 +35,6 @@ for s in "$@"; do
         benchcsr) step benchcsr 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --layout csr ;;
         benchsolo) step benchsolo 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --comm-solo ;;
         benchc1solo) step benchc1solo 300 python bench.py --config C1 --steps 5 --warmup 1 --no-cpu-baseline --comm-solo ;;
-        gridscan) for G in 512 768 896 960 1000 1024; do VTK_SELL_GRID=$G step grid$G 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; done ;;
         profline) step profline 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profline -o run --output-format csv -- python bench.py --prec line --steps 3 --warmup 1 --no-cpu-baseline ;;
         profc4) step profc4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc4 -o run --output-format csv -- python bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 10 ;;
         profmgs) step profmgs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profmgs -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --orth mgs ;;
@@ -58,7 +57,6 @@ for s in "$@"; do
         profsolo) step profsolo 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsolo -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --comm-solo --spmv-reps 5 ;;
         profsoloc2) step profsoloc2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsoloc2 -o run --output-format csv -- python bench.py --config C2 --steps 2 --warmup 1 --no-cpu-baseline --comm-solo --spmv-reps 5 ;;
         profc2) step profc2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profc2 -o run --output-format csv -- python bench.py --config C2 --steps 2 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
-        evab) for E in 1 2 4 1 2 4; do VTK_EV_EVERY=$E step evab_c2_$E 300 python bench.py --config C2 --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 5 || exit $?; python tools/bench_brief.py gpurun_out/evab_c2_$E.log; VTK_EV_EVERY=$E step evab_solo_$E 300 python bench.py --config C2 --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 5 --comm-solo || exit $?; python tools/bench_brief.py gpurun_out/evab_solo_$E.log; done ;;
         profall) for C in C3 C4; do c=$(echo $C | tr C c); A="--config $C --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5";
                  step prof_$c 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline || exit $?;
                  step pmcf_$c 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_$c -o run --output-format csv -- python bench.py $A || exit $?;
@@ -70,10 +68,7 @@ for s in "$@"; do
                step slab_c3_1 300 python bench.py --config C3 --comm-solo --steps 5 --warmup 1 --no-cpu-baseline || exit $?;
                step slab_c4_8 300 python bench.py --config C4 --slab 8 --comm-solo --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
         benchc2full) step benchc2full 600 python bench.py --config C2 ;;
-        abband) for rep in 1 2; do for v in ${BAND_VARIANTS:-cur wg}; do L=vt-precondition_amd/vtkrylov/lib/libvtkrylov.so; ch=1; case $v in cur) ;; nochain) ch=0 ;; *) L=tools/bin/lib_$v/libvtkrylov.so ;; esac; VTK_BAND_CHAIN=$ch VTK_LIB=$L VTK_PROF_PERJ=1 step abband_${v}_$rep 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 5 ${BENCH_ARGS:-} || exit $?; python tools/band_perj.py gpurun_out/abband_${v}_$rep.log; done; done ;;
-        mr4dbg) VTK_DEBUG_BAND=1 step mr4dbg 300 python -u -m pytest tests/test_gpu_multirank.py -x -v -s -k "S2-4" -p no:cacheprovider --timeout 200 --timeout-method thread ;;
         mrlarge) step mrlarge 900 python -u -m pytest tests/test_gpu_multirank_large.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
-        sqband) for impl in wg wave; do VTK_BAND_IMPL=$impl step sqband_$impl 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT -d gpurun_out/sqband_$impl -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --spmv-reps 2 || exit $?; done ;;
         bandtests) step bandtests 600 python -u -m pytest tests/test_gpu_band.py tests/test_gpu_multirank.py tests/test_gpu_large.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
         testsv) step testsv 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         large) step large 600 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;

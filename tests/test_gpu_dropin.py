@@ -170,6 +170,18 @@ def test_grid4_rows_bit_identical(vk_lib, gpu, name):
     out = []
     for A in (G, U):
         M = vk_lib.block_jacobi(A, 8)
+        # the kernel-level pin: w = M^-1 A x from the ring kernel (k_g4_ring, 512- and
+        # 256-row groups, 1 .. 4096 workgroups, the inner-wave sum on and off) is the SELL
+        # grid-row kernel's (k_sell<EPI_PREC>) and the SELL-value kernel's, bit for bit
+        xr = twin.rhs(p.n, seed=0xC0FFEE)
+        with gpu.tuning(g4_ring=0):
+            w_sell = A.precond_matvec(M, xr)
+        with gpu.tuning(g4_ring=0, grid4=0):
+            w_vals = A.precond_matvec(M, xr)
+        assert np.array_equal(w_sell, w_vals)
+        for wgs, gr, fast in ((2048, 512, 1), (2048, 512, 0), (1, 256, 1), (7, 256, 0), (4096, 256, 1), (5, 512, 1)):
+            with gpu.tuning(g4_ring=wgs, g4_gr=gr, g4_fast=fast):
+                assert np.array_equal(A.precond_matvec(M, xr), w_sell), (wgs, gr, fast)
         for orth in ("dcgs2", "mgs"):
             with gpu.tuning(c4_fused=0, g4_ring=0):   # the split step (SELL SpMV + BJ, then the dots)
                 x1, i1, s1 = _solve(vk_lib, A, M, b, orth=orth)

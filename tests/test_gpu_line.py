@@ -346,6 +346,17 @@ def test_line_spmv_fused_into_sweep(vk_lib, gpu, name, seg):
     M = vk_lib.line_jacobi(A, vk_lib.vlasov_line_stride(vk_lib.vlasov_params(p.dim, p.shape)), seg)
     b = twin.rhs(p.n)
     x0 = twin.rhs(p.n, seed=0xB0B) * 1e-3
+    # the kernel-level pin: w = M^-1 A p from the fused kernel (k_line_spmv_dc) is the
+    # two-kernel form's (table SpMV, then the sweeps), bit for bit
+    pv = twin.rhs(p.n, seed=0xC0FFEE)
+    gpu.profile(True)
+    wf = A.precond_matvec(M, pv)
+    assert gpu.profile_read().get("line_dc", {}).get("launches", 0) == 1   # the fused kernel ran
+    gpu.profile(False)
+    with gpu.tuning(line_fuse=0):
+        wu = A.precond_matvec(M, pv)
+    assert np.array_equal(wf, wu)
+    assert np.array_equal(wu, M.matvec(A @ pv))
     for kw in ({}, {"x0": x0}, {"restart": 5}):
         gpu.profile(True)
         xf, i_f = vk_lib.gmres(A, b, rtol=1e-8, M=M, orth="dcgs2", **kw)

@@ -140,3 +140,92 @@ def test_ranks_sharing_one_gpu(tmp_path, case, world, from_host, orth):
     from vtkrylov.comm import check_sequences
     check_sequences([json.loads(str(np.load(tmp_path / f"rank{r}.npz", allow_pickle=False)["commlog"]))
                      for r in range(world)])
+
+
+def _fail_worker(rank, world, port, case, outdir, fail_rank, fail_step, planes):
+    """One rank of a solve in which rank `fail_rank` fails its DCGS2 step `fail_step` (the
+    fail_step test hook: as if that step's launch had been refused), then a clean solve on the
+    same communicator."""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import vtkrylov as vk
+    from oracle import twin
+    ctx = vk.Context(0)
+    hc = ctx.comm_init_host(rank, world)
+    p = twin.CONFIGS[case]
+    if planes:   # whole x planes: the 4D ring step across ranks (halo planes, split launches)
+        align = p.shape[1] * p.shape[2] * p.shape[3]
+        ctx.set_tuning("g4_ring", 64)
+    else:
+        align = p.shape[-1]
+    offs = vk.partition_rows(p.n, world, align)
+    rb, re_ = int(offs[rank]), int(offs[rank + 1])
+    A = vk.vlasov_operator(vk.vlasov_params(p.dim, p.shape, fp32=p.fp32), ctx=ctx, offsets=offs)
+    M = vk.block_jacobi(A, 8)
+    b = twin.rhs(p.n)[rb:re_]
+    if rank == fail_rank:
+        ctx.set_tuning("fail_step", fail_step)
+    t = time.perf_counter()
+    status, msg = 0, ""
+    try:
+        vk.gmres(A, b, rtol=1e-8, M=M, orth="dcgs2")
+    except vk._abi.VtkError as e:
+        status, msg = e.status, str(e)
+    elapsed = time.perf_counter() - t
+    ops_failed = len(hc.log)
+    ctx.set_tuning("fail_step", -1)
+    x2, info2 = vk.gmres(A, b, rtol=1e-8, M=M, orth="dcgs2")
+    st = vk.last_stats()
+    # the kernel-level pin of the step's launch (ADVICE r5): the ring kernel across ranks in the
+    # solver's interior / boundary form == the SELL grid-row SpMV + BJ epilogue, bit for bit
+    xr = twin.rhs(p.n, seed=0xC0FFEE)[rb:re_]
+    w_step = A.precond_matvec(M, xr)
+    with ctx.tuning(g4_ring=0):
+        w_sell = A.precond_matvec(M, xr)
+    np.savez(os.path.join(outdir, f"fail{rank}.npz"), status=status, msg=msg, elapsed=elapsed, x2=x2, info2=info2,
+             iters2=st.inner_iters, band=st.band, rb=rb, re=re_, ops_failed=ops_failed, w_step=w_step, w_sell=w_sell,
+             errors=np.array(hc.errors, dtype=object).astype(str), commlog=json.dumps(hc.log))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world,fail_rank,fail_step,planes", [("S2", 2, 1, 3, False), ("C1", 3, 0, 5, False),
+                                                                   ("S4", 2, 1, 2, True), ("S4", 3, 2, 0, True)])
+def test_peer_failure_is_contained(tmp_path, case, world, fail_rank, fail_step, planes):
+    """A rank whose DCGS2 step fails mid-solve: it votes the failure into the
+    step's all-reduce and keeps issuing the same collectives, so every rank leaves the solve at
+    that step -- the failing one with its own error, the others with VTK_ERR_PEER -- within a
+    bounded time and with the communicator sequence intact; the next solve on the same
+    communicator converges as a clean one does."""
+    import torch.multiprocessing as mp
+
+    import vtkrylov as vk
+    from oracle import coracle, twin
+    mp.spawn(_fail_worker, args=(world, _free_port(), case, str(tmp_path), fail_rank, fail_step, planes),
+             nprocs=world, join=True)
+    p = twin.CONFIGS[case]
+    ip, ix, d = coracle.generate(p)
+    ref = coracle.gmres(ip, ix, d, twin.rhs(p.n), coracle.bj_setup(ip, ix, d, 8), rtol=1e-8)
+    z = [np.load(tmp_path / f"fail{r}.npz", allow_pickle=False) for r in range(world)]
+    xs = np.zeros(p.n)
+    for r in range(world):
+        assert z[r]["errors"].size == 0, z[r]["errors"]
+        st, msg = int(z[r]["status"]), str(z[r]["msg"])
+        if r == fail_rank:
+            assert st == vk._abi.ERR_HIP and "injected failure" in msg, (st, msg)
+        else:
+            assert st == vk._abi.ERR_PEER and "peer rank failed" in msg, (st, msg)
+        assert float(z[r]["elapsed"]) < 30.0
+        assert int(z[r]["band"]) == int(p.dim == 2)
+        assert int(z[r]["info2"]) == 0 and abs(int(z[r]["iters2"]) - ref.inner_iters) <= 1
+        xs[int(z[r]["rb"]):int(z[r]["re"])] = z[r]["x2"]
+        assert np.array_equal(z[r]["w_step"], z[r]["w_sell"]), r
+    assert np.linalg.norm(xs - ref.x) / np.linalg.norm(ref.x) <= 1e-9
+    # every rank left the failed solve after the same collectives, and the whole run (failed solve
+    # + clean solve) is one sequence RCCL could execute
+    assert len({int(q["ops_failed"]) for q in z}) == 1
+    from vtkrylov.comm import check_sequences
+    check_sequences([json.loads(str(q["commlog"])) for q in z])

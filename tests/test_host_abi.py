@@ -27,12 +27,12 @@ def test_library_exports_every_declared_symbol(vk_lib):
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(vk_lib._abi.PROTOTYPES), set(names) ^ set(vk_lib._abi.PROTOTYPES)
-    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 5
+    assert vk_lib._abi.lib().vtk_abi_version() == vk_lib._abi.ABI_VERSION == 6
 
 
 def test_status_strings(vk_lib):
     L = vk_lib._abi.lib()
-    for s in range(0, -8, -1):
+    for s in range(0, -9, -1):
         assert L.vtk_status_string(s).decode() != "unknown status"
 
 

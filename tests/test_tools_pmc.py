@@ -25,6 +25,9 @@ NAMES = {   # rocprofv3 Kernel_Name (argument lists shortened) -> class
     "vtk::k_dc_scalar(double const*, int, double const*, int)": "dc_scalar",
     "vtk::k_xupdate(double const*, double const*, double const*, long)": "xupdate",
     "void vtk::k_line_apply<25, true, true>(vtk::LineOp, double const*)": "line_dc",
+    "void vtk::k_line_spmv_dc<25>(vtk::LineOp, double const*, double const*, double*, int, int const*, int, vtk::LineDc)": "line_dc",
+    "void vtk::k_line_spmv_dc<8>(vtk::LineOp, double const*)": "line_dc",
+    "void vtk::k_line_apply<25, true, false>(vtk::LineOp, double const*, double*)": "line_apply",
 }
 
 

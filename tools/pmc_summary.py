@@ -39,7 +39,9 @@ CLASSES = {   # bench/profile class -> demangled-name prefix (regex) in rocprofv
     "spmv_csr": r"void vtk::k_spmv<(double|float), false, 0, 1",
     "spmv_bj_dc_csr": r"void vtk::k_spmv<(double|float), false, 4, 8",
     "dc_dots": r"void vtk::k_dc_dots(_rows<\d+>)?\(",
-    "line_dc": r"void vtk::k_line_apply<\d+, (true|false), true>",
+    # the line path's DCGS2 step: the sweep with its dots (k_line_apply<SEG, COMPACT, true>) or,
+    # one rank with canonical rows, the fused SpMV + sweep + dots (k_line_spmv_dc<SEG>, round 5)
+    "line_dc": r"void vtk::k_line_(apply<\d+, (true|false), true>|spmv_dc<\d+>)",
     "line_apply": r"void vtk::k_line_apply<\d+, (true|false)(, false)?>",
     "dc_update": "void vtk::k_dc_update<",
     "dc_scalar": "vtk::k_dc_scalar(",

@@ -1,7 +1,11 @@
 """In-process A/B of the plain SpMV (vtk_spmv, the measured half of the metric) over context
 tuning settings: one operator, alternating settings, HIP-event timing on the library's stream.
 
-    python tools/spmv_ab.py --config C3 --settings "sell_canon=0;sell_canon=1;grid4=0"
+    python tools/spmv_ab.py --config C3 --settings "layout=sell;layout=csr"
+
+A setting is `layout=sell|csr` (vtk_csr_set_layout: the switch that reaches vtk_spmv; the
+solver's tuning keys -- sell_canon, grid4, ... -- are compiled out of the plain SpMV)
+or a context tuning key=value, comma-separated.
 
 Prints one JSON line: per setting the per-launch microseconds of every round and their median,
 and the algorithmic GB/s (layout bytes + x + y)."""
@@ -21,7 +25,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "vt-precondition_amd")]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--settings", default="sell_canon=0;sell_canon=1")
+    ap.add_argument("--settings", default="layout=sell;layout=csr")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=50)
     a = ap.parse_args()
@@ -39,14 +43,18 @@ def main():
     torch.cuda.synchronize()
     lib = vk._abi.lib()
     stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=dev)
-    sets = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv) for s in a.settings.split(";")]
-    nbytes = A.layout_info()["matrix_bytes"] + 16 * A.n_local
+    sets = [dict((kv.split("=")[0], kv.split("=")[1]) for kv in s.split(",") if kv) for s in a.settings.split(";")]
+    nbytes = {}
     times = {i: [] for i in range(len(sets))}
     for r in range(a.rounds + 1):
         order = range(len(sets)) if r % 2 == 0 else reversed(range(len(sets)))
         for i in order:
             for k, v in sets[i].items():
-                ctx.set_tuning(k, v)
+                if k == "layout":
+                    A.set_layout(v)
+                else:
+                    ctx.set_tuning(k, int(v))
+            nbytes[i] = A.layout_info()["matrix_bytes"] + 16 * A.n_local
             for _ in range(3):
                 vk._abi.check(lib.vtk_spmv(A.handle, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), 1))
             ctx.synchronize()
@@ -62,10 +70,11 @@ def main():
             if y0 is None:
                 y0 = yh
             assert np.array_equal(yh, y0), "SpMV bits changed with a tuning setting"
-    out = {"config": a.config, "bytes": nbytes, "settings": {}}
+    out = {"config": a.config, "settings": {}}
     for i, s in enumerate(sets):
         med = statistics.median(times[i])
-        out["settings"][a.settings.split(";")[i]] = {"median_us": med, "gbs": nbytes / med / 1e3, "us": times[i]}
+        out["settings"][a.settings.split(";")[i]] = {"median_us": med, "bytes": nbytes[i], "gbs": nbytes[i] / med / 1e3,
+                                                    "us": times[i]}
     print(json.dumps(out))
 
 

@@ -49,8 +49,10 @@ int fail(vtk_ctx *c, int code, const std::string &msg) {
 #define NCCLCHK(c, x)                                                                        \
     do {                                                                                     \
         ncclResult_t r_ = (x);                                                               \
-        if (r_ != ncclSuccess)                                                               \
+        if (r_ != ncclSuccess) {                                                             \
+            if (c) (c)->comm_broken = true;                                                  \
             return fail((c), VTK_ERR_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+        }                                                                                    \
     } while (0)
 
 #define TRY(x)                          \
@@ -82,6 +84,7 @@ constexpr TuneKey TUNE_KEYS[] = {
     {"prof_perj", &Tuning::prof_perj}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring},
     {"g4_gr", &Tuning::g4_gr}, {"g4_fast", &Tuning::g4_fast}, {"line_fuse", &Tuning::line_fuse}, {"cyc_ring", &Tuning::cyc_ring},
+    {"fail_step", &Tuning::fail_step},
 };
 // switches of earlier rounds whose alternative lost its A/B: an environment that
 // still sets one is told once that it no longer has an effect
@@ -842,9 +845,9 @@ int band_check_all(vtk_csr *A, int64_t L) {
     if (c->dist) {
         // the agreement runs even after a local failure: every rank joins the same collective
         double mine = rc == VTK_OK ? 0.0 : 1.0, bad = 0.0;
-        HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        TRY(comm_allreduce(c, &c->d_scal[DC_NQ], 1));
-        HIPCHK(c, hipMemcpyAsync(&bad, &c->d_scal[DC_NQ], sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ + 2], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        TRY(comm_allreduce(c, &c->d_scal[DC_NQ + 2], 1));
+        HIPCHK(c, hipMemcpyAsync(&bad, &c->d_scal[DC_NQ + 2], sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (rc == VTK_OK && bad != 0.0) rc = VTK_ERR_ARG;
     }
@@ -908,16 +911,17 @@ int line_len_candidate(vtk_csr *A, int64_t &L) {
     };
     const int lrc = local();
     if (lrc != VTK_OK) L = -1;
+    if (c->dist && c->world > 120) {
+        // the agreement below gathers into the context's scalar scratch (room for 120 ranks, no
+        // allocation that could fail on one rank only).  Beyond that every rank
+        // skips the detection alike -- no collective, the plain path; vtk_csr_set_line_band
+        // still sets the band explicitly
+        L = 0;
+        return lrc;
+    }
     if (c->dist) {
-        // the context's scalar scratch (no allocation that could fail on one rank only) for up to
-        // 120 ranks
         const int W = c->world;
-        DBuf own;
         int64_t *mine = reinterpret_cast<int64_t *>(c->d_scal + 128);
-        if (W > 120) {
-            if (dalloc(c, own, (size_t)(W + 1) * sizeof(int64_t)) != VTK_OK) return fail(c, VTK_ERR_NOMEM, "line band detection: allgather buffer");
-            mine = own.as<int64_t>();
-        }
         HIPCHK(c, hipMemcpyAsync(mine, &L, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
         TRY(comm_allgather_i64(c, mine, mine + 1, 1));
         std::vector<int64_t> h((size_t)W);
@@ -1058,7 +1062,32 @@ struct Solver {
     int band_grid(int j, int opt) const { return (opt & 2) && j <= BAND_J3 && band_G3 > 0 ? band_G3 : band_G; }
     double *w3 = nullptr;
     double *ghost = nullptr, *gsend = nullptr, *grecv = nullptr;   // distributed band step
+    // across ranks: the first launch of this rank that failed (soft_launch), and the fail_step
+    // test hook still to fire in this solve
+    int local_rc = VTK_OK;
+    bool fail_pending = false;
 };
+
+// A launch of the solve that failed.  On one rank: the error returns at once.  Across ranks the
+// peers are already inside this step's collectives, so returning would leave them blocked: the
+// rank records its error, sets its failure vote (d_scal[DC_VOTE + 1], summed into the step's
+// all-reduce by k_dc_finalize) and goes on issuing the same launches and collectives; the vote
+// stops every rank's cycle at the same step and vtk_gmres returns the error there (VTK_ERR_PEER
+// on the other ranks).  (Pattern: the reference's step runner turns a step's exception into a
+// return code, precondition_setup/vtsetup/vt_precondition.py:66-79.)
+int soft_launch(Solver &s, hipError_t e, const char *what) {
+    vtk_ctx *c = s.c;
+    if (e == hipSuccess) return VTK_OK;
+    const int code = e == hipErrorOutOfMemory ? VTK_ERR_NOMEM : VTK_ERR_HIP;
+    const std::string msg = std::string(what) + ": " + hipGetErrorString(e);
+    if (!c->dist) return fail(c, code, msg);
+    if (s.local_rc == VTK_OK) {
+        s.local_rc = fail(c, code, msg + " (the ranks left the solve together at the next all-reduce)");
+        HIPCHK(c, hipMemsetAsync(&c->d_scal[DC_VOTE + 1], 1, sizeof(double), c->stream));
+    }
+    return VTK_OK;
+}
+#define SOFT(x) TRY(soft_launch(s, (x), #x))
 
 // w = M^-1 A v (fused when the tiles allow), partials: part[0] = w^2 (h0), part[1] = v0*w
 // the x-line ring with the solver's epilogues (k_lsv_ring_epi): one rank, line-separable canonical
@@ -1082,6 +1111,25 @@ bool g4_resid_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M) {
     return A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && A->use_sell &&
            A->sell.uniform_w > 8 && M && M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr &&
            g4_ring_fits(A->g4, A->n_local, c->tune.g4_gr);
+}
+
+// the line path's table SpMV: the line-separable, canonical rows' tables (tunings band_lsv,
+// sell_canon) of a uniform width-5 SELL copy; across ranks with the ghost lines
+bool line_lsv_ok(vtk_ctx *c, const vtk_csr *A) {
+    return A->d_lsv && A->band_L > 0 && c->tune.band_lsv && A->use_sell && A->sell.uniform_w == 5 && A->sell.d_pk &&
+           A->sell.n_wide == 0 && (!c->dist || A->band_ghost);
+}
+// ... and the SpMV inside the sweep kernel (k_line_spmv_dc, tuning line_fuse): one rank, canonical
+// rows, compact factors over the whole slab
+bool line_fuse_ok(vtk_ctx *c, const vtk_csr *A, const vtk_prec *M) {
+    if (!M || M->kind != VTK_PREC_LINE || !line_lsv_ok(c, A) || !A->lsv_canon || !c->tune.sell_canon ||
+        !c->tune.line_fuse || c->dist)
+        return false;
+    const LineOp &lo = M->line;
+    const int64_t n = A->n_local;
+    return lo.seg >= 1 && lo.seg <= 32 && lo.compact && lo.stride == A->band_L && lo.row0 == 0 && lo.n == n &&
+           lo.j0 == 0 && lo.jn == lo.stride && lo.ac && lo.i_lo == 0 && lo.i_hi == n / lo.stride - 1 &&
+           n / lo.stride >= 3;
 }
 
 int precond_matvec(Solver &s, const double *v, double *w, const int *stop, int col, Red &h0, Red &d0,
@@ -1151,9 +1199,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     const bool line_dc = s.M && s.M->kind == VTK_PREC_LINE && s.M->line.seg >= 1 &&
                          s.M->line.seg <= 32 && s.G <= GMAX;
     // line path on a line-separable operator: the SpMV from the tables (VTK_BAND_LSV=0: SELL)
-    const bool line_lsv = line_dc && s.A->d_lsv && s.A->band_L > 0 && c->tune.band_lsv && s.A->use_sell &&
-                          s.A->sell.uniform_w == 5 && s.A->sell.d_pk && s.A->sell.n_wide == 0 &&
-                          (!c->dist || s.A->band_ghost);
+    const bool line_lsv = line_dc && line_lsv_ok(c, s.A);
     const Tiles *ft = s.M ? &s.M->tiles : &s.A->tiles;
     const double b_csr = matrix_bytes(s.A);
     const double b_lsv = b_csr - 8.0 * (double)s.A->sell.entries + 8.0 * (double)n;
@@ -1169,7 +1215,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     auto reduce_step = [&](int j, const double *w, int tag, int cnt, hipEvent_t ev_ar = nullptr) -> int {
         if (cnt == 0) {
             Prof pf(c, "dc_dots", tag, n8 * (j + (w ? 2 : 1)));
-            HIPCHK(c, launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, tag, c->stream));
+            SOFT(launch_dc_dots(s.V, s.ld, j, w, n, s.dcpart, s.G, stop, tag, c->stream));
             cnt = s.G;
         }
         const double *part = s.dcpart;
@@ -1177,8 +1223,8 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             { Prof pf(c, "dc_finalize", tag, 0.0);
               HIPCHK(c, launch_dc_finalize(s.dcpart, cnt, j, w != nullptr, c->d_scal, stop, tag, c->stream)); }
             {
-                Prof pf(c, "allreduce", tag, 8.0 * DC_NQ);
-                TRY(comm_allreduce(c, c->d_scal, DC_NQ));
+                Prof pf(c, "allreduce", tag, 8.0 * DC_NQV);
+                TRY(comm_allreduce(c, c->d_scal, DC_NQV));   // the dots + the failure vote
             }
             if (ev_ar) HIPCHK(c, hipEventRecord(ev_ar, c->stream));
             part = nullptr;
@@ -1223,7 +1269,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
             const bool hl = s.A->band_ghost;
-            HIPCHK(c, launch_lsv_ring_epi(EPI_PREC_DC, s.A->d_lsv, pj, nullptr, s.M->d_tri + s.M->tri_ld, s.w, nullptr,
+            SOFT(launch_lsv_ring_epi(EPI_PREC_DC, s.A->d_lsv, pj, nullptr, s.M->d_tri + s.M->tri_ld, s.w, nullptr,
                                           nullptr, s.dcpart, n, (int)s.A->band_L, c->tune.cyc_ring, stop, j, &cnt,
                                           c->stream, hl ? s.A->d_halo : nullptr, s.A->band_lblk, s.A->band_xord));
         } else if (fused && bj_split(s.M)) {
@@ -1240,7 +1286,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             if (exch) TRY(halo_exchange_async(s.A, pj));
             {
                 Prof pf(c, "spmv_bj_dc", j, b_step * std::min(1.0, f_in));
-                HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
+                SOFT(launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             }
             // the all-reduce below stays behind this rank's exchange on every rank (one order
             // of RCCL operations on the communicator)
@@ -1248,7 +1294,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             cnt = spmv_grid(in);
             if (has_bd) {
                 Prof pf(c, "spmv_bj_dc_bd", j, b_step * std::max(0.0, 1.0 - f_in));
-                HIPCHK(c, launch_spmv_dc(bd, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart + spmv_grid(in), stop, j,
+                SOFT(launch_spmv_dc(bd, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart + spmv_grid(in), stop, j,
                                          c->stream));
                 cnt += spmv_grid(bd);
             }
@@ -1256,34 +1302,32 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             TRY(halo_exchange(s.A, pj));
             Prof pf(c, "spmv_bj_dc", j, b_step);
             const SpmvIn in = lsv_in(spmv_in(s.A, ft, pj), s.A);
-            HIPCHK(c, launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
+            SOFT(launch_spmv_dc(in, s.w, bj_op(s.M), s.V, s.ld, j, s.dcpart, stop, j, c->stream));
             cnt = spmv_grid(in);
         } else if (line_dc) {
             // line path: SpMV, then the line sweeps with the step's dots fused behind them
             TRY(halo_exchange(s.A, pj));
             const LineOp &lo = s.M->line;
-            if (line_canon && c->tune.line_fuse && !c->dist && lo.compact && lo.stride == s.A->band_L &&
-                lo.row0 == 0 && lo.n == n && lo.j0 == 0 && lo.jn == lo.stride && lo.ac && lo.i_lo == 0 &&
-                lo.i_hi == n / lo.stride - 1 && n / lo.stride >= 3 && lo.seg <= 32) {
+            if (line_canon && line_fuse_ok(c, s.A, s.M)) {
                 // one rank: the SpMV inside the sweep kernel (y never stored)
                 Prof pf(c, "line_dc", j, b_inv + 8.0 * (double)n + n8 * (j + 2));   // m, D, p, w, V_j
-                HIPCHK(c, launch_line_spmv_dc(lo, s.A->d_lsv, pj, s.w, s.V, s.ld, j, s.dcpart, s.G, stop, j, c->stream));
+                SOFT(launch_line_spmv_dc(lo, s.A->d_lsv, pj, s.w, s.V, s.ld, j, s.dcpart, s.G, stop, j, c->stream));
                 cnt = s.G;
             } else if (line_lsv) {
                 // line-separable values: 12 B of matrix per row (codes + diagonal)
                 Prof pf(c, "spmv_lsv", j, (line_canon ? 8.0 * (double)n : b_lsv) + 2 * n8);
-                HIPCHK(c, launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
+                SOFT(launch_lsv_spmv(s.A->sell.d_pk, s.A->sell.d_dict, s.A->d_lsv, pj, c->dist ? s.A->d_halo : nullptr,
                                           s.tmp, n, (int)s.A->band_L, s.A->band_ghost ? s.A->band_lblk : -1, stop, j,
                                           c->stream, line_canon ? 1 : 0, 8192, c->tune.lsv_ring,
                                           s.A->band_ghost ? s.A->band_xord : 0));
             } else {
                 Prof pf(c, "spmv", j, b_csr + 2 * n8);
-                HIPCHK(c, launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
+                SOFT(launch_spmv(spmv_in(s.A, &s.A->tiles, pj), EPI_PLAIN, s.tmp, nullptr, BjOp{}, nullptr, nullptr,
                                       nullptr, stop, j, c->stream));
             }
             if (!cnt) {
                 Prof pf(c, "line_dc", j, b_inv + n8 * (j + 3));   // r, m, w, p, V_j
-                HIPCHK(c, launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream));
+                SOFT(launch_line_dc(s.M->line, s.tmp, s.w, s.V, s.ld, j, pj, s.dcpart, s.G, stop, j, c->stream));
                 cnt = s.G;
             }
         } else if (ring4) {
@@ -1301,7 +1345,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 TRY(halo_exchange(s.A, pj));
                 Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring);
                 int grid = 0;
-                HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_gr,
+                SOFT(launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring, c->tune.g4_gr,
                                          dc ? &dd : nullptr, &grid, stop, j, c->stream, 0, -1, 0,
                                          c->tune.g4_fast));
                 if (dc) cnt = grid;
@@ -1322,7 +1366,7 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 {
                     Prof pf(c, dc ? "spmv_bj_dc" : "spmv_bj", j, b_ring * (double)(gi_hi - gi_lo) * G / std::max<double>(1.0, (double)n));
                     if (gi_hi > gi_lo)
-                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
+                        SOFT(launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                                  c->tune.g4_gr, dc ? &dd : nullptr, &gin, stop, j, c->stream, (int)gi_lo,
                                                  (int)gi_hi, per, c->tune.g4_fast));
                 }
@@ -1330,12 +1374,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
                 {
                     Prof pf(c, "spmv_bj_bd", j, b_ring * std::max(0.0, 1.0 - (double)(gi_hi - gi_lo) * G / std::max<double>(1.0, (double)n)));
                     dd.part_off = gin;
-                    HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
+                    SOFT(launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                              c->tune.g4_gr, dc ? &dd : nullptr, &gb0, stop, j, c->stream, 0,
                                              (int)(gi_hi > gi_lo ? gi_lo : ng), per, c->tune.g4_fast));
                     if (gi_hi > gi_lo) {
                         dd.part_off = gin + gb0;
-                        HIPCHK(c, launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
+                        SOFT(launch_g4_ring(s.A->g4, pj, halo, mt, s.w, n, s.A->fp32, c->tune.g4_ring,
                                                  c->tune.g4_gr, dc ? &dd : nullptr, &gb1, stop, j, c->stream, (int)gi_hi,
                                                  (int)ng, per, c->tune.g4_fast));
                     }
@@ -1351,17 +1395,21 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
         // the RCCL operations never overlap; the exchange overlaps the scalar step); the band
         // step waits for them
         const bool ghost_x = band && s.ghost && j <= m - 2;
+        if (s.fail_pending && j == c->tune.fail_step) {   // test hook: as if this step's launch failed
+            s.fail_pending = false;
+            TRY(soft_launch(s, hipErrorLaunchFailure, "injected failure (tuning fail_step)"));
+        }
         TRY(reduce_step(j, w_cur, j, cnt, ghost_x && c->dist ? c->ev_pack : nullptr));
         if (ghost_x && !c->dist) HIPCHK(c, hipEventRecord(c->ev_pack, c->stream));
         if (ghost_x) {
             vtk_csr *A = s.A;
             const int L = (int)A->band_L;
             HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_pack, 0));
-            HIPCHK(c, launch_ghost_pack(s.V, s.ld, j, w_cur, n, L, s.gsend, A->band_off_first, A->band_off_last,
+            SOFT(launch_ghost_pack(s.V, s.ld, j, w_cur, n, L, s.gsend, A->band_off_first, A->band_off_last,
                                         c->comm_stream));
             TRY(comm_alltoallv(c, s.gsend, A->band_scnt, A->band_soff, s.grecv, A->band_rcnt, A->band_roff, ncclDouble,
                                sizeof(double), c->comm_stream));
-            HIPCHK(c, launch_ghost_unpack(s.grecv, A->band_off_left, A->band_off_right, j, m, L, s.ghost, c->comm_stream));
+            SOFT(launch_ghost_unpack(s.grecv, A->band_off_left, A->band_off_right, j, m, L, s.ghost, c->comm_stream));
             HIPCHK(c, hipEventRecord(c->ev_halo, c->comm_stream));
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
         }
@@ -1404,10 +1452,10 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
             a.lsv = band_lsv ? s.A->d_lsv : nullptr;
             a.canon = band_lsv && s.A->lsv_canon && band_canon ? 2 : 0;   // 2: the straight-line SpMV per line order
             a.opt = band_opt;
-            HIPCHK(c, launch_band_step(a, s.band_grid(j, a.opt), s.A->sell.uniform_w, c->stream));
+            SOFT(launch_band_step(a, s.band_grid(j, a.opt), s.A->sell.uniform_w, c->stream));
         } else {
             Prof pf(c, "dc_update", j, n8 * (j + 4));
-            HIPCHK(c, launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1, c->stream));
+            SOFT(launch_dc_update(s.V, s.ld, j, w_cur, n, s.cf, s.G, ds, s.x, s.H, s.S, m, fused ? 0 : 1, c->stream));
         }
         // throttle: an event every ev_every steps (each record costs the stream a few us); the
         // host waits for the event LOOKAHEAD or more steps back and acts on a stop the device
@@ -1482,10 +1530,10 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
                                m >= 2 && m <= 20;
     if (c->dist && band_possible) {
         double mine = s.band ? 0.0 : 1.0;
-        HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        TRY(comm_allreduce(c, &c->d_scal[DC_NQ], 1));
+        HIPCHK(c, hipMemcpyAsync(&c->d_scal[DC_NQ + 2], &mine, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        TRY(comm_allreduce(c, &c->d_scal[DC_NQ + 2], 1));
         double off = 0.0;
-        HIPCHK(c, hipMemcpyAsync(&off, &c->d_scal[DC_NQ], sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&off, &c->d_scal[DC_NQ + 2], sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (off != 0.0) s.band = false;
     }
@@ -1534,6 +1582,8 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
     hs->stop_col = BIG_COL;
     hs->xup_tag = -1;
     HIPCHK(c, hipMemcpyAsync(ds, hs, sizeof(GmresState), hipMemcpyHostToDevice, c->stream));
+    if (c->dist) HIPCHK(c, hipMemsetAsync(&c->d_scal[DC_VOTE + 1], 0, sizeof(double), c->stream));   // no failure yet
+    s.fail_pending = c->tune.fail_step >= 0;
     int rc;
     const double n8 = 8.0 * n;
     const double b_pc = bj_row_bytes(M) * n + 2 * n8;
@@ -1578,7 +1628,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             dd.p0 = prr;
             dd.p1 = prz;
             int g = 0;
-            HIPCHK(c, launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
+            SOFT(launch_g4_ring(A->g4, x, A->g4.lblk >= 0 ? A->d_halo : nullptr, M->d_tri + M->tri_ld, s.V, n, A->fp32,
                                      c->tune.g4_ring, c->tune.g4_gr, &dd, &g, nullptr,
                                      0, c->stream, 0, -1, 0, c->tune.g4_fast));
             TRY(pad_partials(c, prr, prz, g));
@@ -1589,7 +1639,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         } else if (fres && M && cyc_ring_ok(c, A, M, true)) {   // the same through the x-line ring
             Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
             int g = 0;
-            HIPCHK(c, launch_lsv_ring_epi(EPI_RESID_PREC, A->d_lsv, x, b, M->d_tri + M->tri_ld, s.V, prr, prz, nullptr,
+            SOFT(launch_lsv_ring_epi(EPI_RESID_PREC, A->d_lsv, x, b, M->d_tri + M->tri_ld, s.V, prr, prz, nullptr,
                                           n, (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream,
                                           A->band_ghost ? A->d_halo : nullptr, A->band_lblk, A->band_xord));
             TRY(pad_partials(c, prr, prz, g));
@@ -1599,7 +1649,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             TRY(rc2);
         } else if (fres) {
             Prof pf(c, "spmv_resid_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 3 * n8);
-            HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, rtiles, x), A), EPI_RESID_PREC, s.V, b, bj_op(M),
+            SOFT(launch_spmv(lsv_in(spmv_in(A, rtiles, x), A), EPI_RESID_PREC, s.V, b, bj_op(M),
                                   nullptr, prr, prz, nullptr, 0, c->stream));
             rr = reduce(c, prr, spmv_grid(rin0), rc2);
             TRY(rc2);
@@ -1608,7 +1658,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         } else if (cyc_ring_ok(c, A, M, false)) {
             Prof pf(c, "spmv_resid", -1, solver_matrix_bytes(A) + 3 * n8);
             int g = 0;
-            HIPCHK(c, launch_lsv_ring_epi(EPI_RESID, A->d_lsv, x, b, nullptr, s.r, prr, nullptr, nullptr, n,
+            SOFT(launch_lsv_ring_epi(EPI_RESID, A->d_lsv, x, b, nullptr, s.r, prr, nullptr, nullptr, n,
                                           (int)A->band_L, c->tune.cyc_ring, nullptr, 0, &g, c->stream,
                                           A->band_ghost ? A->d_halo : nullptr, A->band_lblk, A->band_xord));
             TRY(pad_partials(c, prr, nullptr, g));
@@ -1616,7 +1666,7 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
             TRY(rc2);
         } else {
             Prof pf(c, "spmv_resid", -1, solver_matrix_bytes(A) + 3 * n8);
-            HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, &A->tiles, x), A), EPI_RESID, s.r, b, BjOp{}, nullptr, prr, nullptr, nullptr, 0, c->stream));
+            SOFT(launch_spmv(lsv_in(spmv_in(A, &A->tiles, x), A), EPI_RESID, s.r, b, BjOp{}, nullptr, prr, nullptr, nullptr, 0, c->stream));
             rr = reduce(c, prr, spmv_grid(pin0), rc2);
             TRY(rc2);
         }
@@ -1671,12 +1721,12 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         Red rv = rz;
         if (!fres && !(it == 0 && r_is_b)) {
             { Prof pf(c, prec_cls(M), -1, b_pc);
-              HIPCHK(c, launch_bj_apply(bj_op(M), n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
+              SOFT(launch_bj_apply(bj_op(M), n, s.r, s.V, nullptr, s.part[0], nullptr, s.G, nullptr, 0, c->stream)); }
             rv = reduce(c, s.part[0], s.G, rc);
             TRY(rc);
         }
         { Prof pf(c, "scale0", -1, 2 * n8);
-          HIPCHK(c, launch_scale0(rv, s.V, n, s.S, m, ds, s.G, c->stream)); }
+          SOFT(launch_scale0(rv, s.V, n, s.S, m, ds, s.G, c->stream)); }
         const int *stop = &ds->stop_col;
         *mirror = BIG_COL;
         int enq = 0;
@@ -1693,12 +1743,12 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
                 double *po = s.part[2 + (k & 1)];
                 const double *vn = k < col ? s.V + (size_t)(k + 1) * s.ld : nullptr;
                 { Prof pf(c, "mgs", col, (vn ? 4 : 3) * n8);
-                  HIPCHK(c, launch_mgs(cur, s.H + (size_t)col * (m + 1) + k, s.w, s.V + (size_t)k * s.ld, vn, n, po, s.G, stop, col, c->stream)); }
+                  SOFT(launch_mgs(cur, s.H + (size_t)col * (m + 1) + k, s.w, s.V + (size_t)k * s.ld, vn, n, po, s.G, stop, col, c->stream)); }
                 cur = reduce(c, po, s.G, rc);
                 TRY(rc);
             }
             { Prof pf(c, "tail", col, 2 * n8);
-              HIPCHK(c, launch_tail(h0, cur, s.w, s.V + (size_t)(col + 1) * s.ld, n, col, m, s.H, s.S, s.giv, ds, c->d_stop, s.G, c->stream)); }
+              SOFT(launch_tail(h0, cur, s.w, s.V + (size_t)(col + 1) * s.ld, n, col, m, s.H, s.S, s.giv, ds, c->d_stop, s.G, c->stream)); }
             HIPCHK(c, hipEventRecord(ev[col % (LOOKAHEAD + 1)], c->stream));
             enq = col + 1;
             if (col >= LOOKAHEAD) {
@@ -1714,10 +1764,24 @@ int run_gmres(vtk_csr *A, vtk_prec *M, const double *b, double *x, double rtol, 
         // x += y @ V[:col+1] (:799-814), r = b - A x, rnorm (:816-817)
         const size_t xup_idx = c->prof_pending.size();
         { Prof pf(c, "xupdate", -1, 0.0);   // bytes set once the stop column is known
-          HIPCHK(c, launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream)); }
+          SOFT(launch_xupdate(s.H, s.S, s.V, s.ld, x, n, m, ds, s.G, c->stream)); }
         TRY(residual());
+        // across ranks: the cycle's failure vote (a launch of some rank failed in this cycle; the
+        // per-step vote has already stopped the Arnoldi steps at the same step on every rank)
+        double vote = 0.0;
+        if (c->dist) {
+            TRY(comm_allreduce(c, &c->d_scal[DC_VOTE + 1], 1));
+            HIPCHK(c, hipMemcpyAsync(&vote, &c->d_scal[DC_VOTE + 1], sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        }
         HIPCHK(c, hipMemcpyAsync(hs, ds, sizeof(GmresState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (vote != 0.0) {
+            prof_flush(c);
+            if (s.local_rc != VTK_OK) return s.local_rc;
+            return fail(c, VTK_ERR_PEER, "a peer rank failed in restart cycle " + std::to_string(it) +
+                                             (hs->breakdown == PEER_FAILED ? " at Arnoldi step " + std::to_string(hs->stop_col + 1) : std::string()) +
+                                             "; every rank left the solve there");
+        }
         const int last = hs->stop_col < m ? hs->stop_col : m - 1;
         if (c->prof_on) {
             const double xb = n8 * (last + 1) + 2 * n8;   // V[0..last] (or V_last and p_last), x in/out
@@ -1809,7 +1873,8 @@ int vtk_ctx_create(int device, vtk_ctx **out) {
 void vtk_ctx_destroy(vtk_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    // a communicator whose collective failed may have peers blocked in it: abort, do not destroy
+    if (c->comm) (void)(c->comm_broken ? ncclCommAbort(c->comm) : ncclCommDestroy(c->comm));
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     prof_flush(c);
     for (auto e : c->prof_pool) (void)hipEventDestroy(e);
@@ -2235,6 +2300,80 @@ int vtk_linejacobi_get_compact(vtk_prec *M, int *in_use, int *available) {
 }
 
 int vtk_prec_apply(vtk_prec *M, const double *r, double *z, int kind) { return vtk_bjacobi_apply(M, r, z, kind); }
+
+// w = M^-1 A x through the launch the solver's split DCGS2 step uses for this operator (ADVICE r5:
+// the kernel-level pin of k_g4_ring against k_sell<EPI_PREC>): the 4D ring kernel when it applies
+// -- across ranks in the solver's form, interior groups while the halo planes travel, then the
+// first / last planes' groups --, else the SELL / CSR SpMV with the BJ epilogue, else SpMV + apply
+int vtk_precond_matvec(vtk_csr *A, vtk_prec *M, const double *x, double *w, int kind) {
+    if (!A || !x || !w || (M && M->A != A)) return fail(A ? A->ctx : nullptr, VTK_ERR_ARG, "vtk_precond_matvec: bad arguments");
+    vtk_ctx *c = A->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t n = A->n_local;
+    Staged sx, sw;
+    TRY(stage_in(c, x, n, kind, sx));
+    TRY(stage_in(c, kind == VTK_PTR_DEVICE ? w : nullptr, n, kind, sw));
+    const bool ring = A->d_g4tab && c->tune.grid4 && c->tune.g4_ring > 0 && A->use_sell && M &&
+                      M->kind == VTK_PREC_BJACOBI && M->bs == 8 && bj_op(M).tri != nullptr &&
+                      g4_ring_fits(A->g4, n, c->tune.g4_gr);
+    double *p0 = c->d_part, *p1 = c->d_part + GMAX;
+    if (ring) {
+        const double *halo = A->g4.lblk >= 0 ? A->d_halo : nullptr;
+        const double *mt = M->d_tri + M->tri_ld;
+        Prof pf(c, "spmv_bj", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 16.0 * n);
+        if (!halo) {
+            TRY(halo_exchange(A, sx.d));
+            HIPCHK(c, launch_g4_ring(A->g4, sx.d, nullptr, mt, sw.d, n, A->fp32, c->tune.g4_ring, c->tune.g4_gr, nullptr,
+                                     nullptr, nullptr, 0, c->stream, 0, -1, 0, c->tune.g4_fast));
+        } else {   // dcgs2_cycle's split form (mode 0)
+            const int G = g4_ring_group(c->tune.g4_gr);
+            const int64_t S4 = (int64_t)A->g4.Ny * A->g4.Nvx * A->g4.Nvy, ng = (n + G - 1) / G;
+            int64_t gi_lo = (S4 + G - 1) / G, gi_hi = (n - S4) / G;
+            if (gi_hi <= gi_lo) gi_lo = gi_hi = 0;
+            const int per = (int)g4_ring_per(ng, S4, G, std::max(1, c->tune.g4_ring));
+            TRY(halo_exchange_async(A, sx.d));
+            if (gi_hi > gi_lo)
+                HIPCHK(c, launch_g4_ring(A->g4, sx.d, halo, mt, sw.d, n, A->fp32, c->tune.g4_ring, c->tune.g4_gr, nullptr,
+                                         nullptr, nullptr, 0, c->stream, (int)gi_lo, (int)gi_hi, per, c->tune.g4_fast));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+            HIPCHK(c, launch_g4_ring(A->g4, sx.d, halo, mt, sw.d, n, A->fp32, c->tune.g4_ring, c->tune.g4_gr, nullptr,
+                                     nullptr, nullptr, 0, c->stream, 0, (int)(gi_hi > gi_lo ? gi_lo : ng), per,
+                                     c->tune.g4_fast));
+            if (gi_hi > gi_lo)
+                HIPCHK(c, launch_g4_ring(A->g4, sx.d, halo, mt, sw.d, n, A->fp32, c->tune.g4_ring, c->tune.g4_gr, nullptr,
+                                         nullptr, nullptr, 0, c->stream, (int)gi_hi, (int)ng, per, c->tune.g4_fast));
+        }
+    } else if (line_fuse_ok(c, A, M)) {
+        // the line step's form: y = A x formed inside the sweep kernel (k_line_spmv_dc; its step-0
+        // dots go to a scratch), the ADVICE r5 pin of the fused kernel against SpMV + sweeps below
+        DBuf part;
+        TRY(dalloc(c, part, (size_t)DC_NQ * GMAX * sizeof(double)));
+        Prof pf(c, "line_dc", -1, bj_row_bytes(M) * n + 24.0 * n);
+        HIPCHK(c, launch_line_spmv_dc(M->line, A->d_lsv, sx.d, sw.d, sx.d, n, 0, part.as<double>(), vector_grid(n),
+                                      nullptr, 0, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));   // part is freed on return
+    } else if (!M || bj_fused(M)) {
+        TRY(halo_exchange(A, sx.d));
+        Prof pf(c, M ? "spmv_bj" : "spmv_w", -1, solver_matrix_bytes(A) + bj_row_bytes(M) * n + 16.0 * n);
+        HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, M ? &M->tiles : &A->tiles, sx.d), A), EPI_PREC, sw.d, nullptr,
+                              M ? bj_op(M) : BjOp{}, nullptr, p0, p1, nullptr, 0, c->stream));
+    } else {
+        TRY(halo_exchange(A, sx.d));
+        DBuf t;
+        TRY(dalloc(c, t, std::max<int64_t>(n, 1) * sizeof(double)));
+        HIPCHK(c, launch_spmv(lsv_in(spmv_in(A, &A->tiles, sx.d), A), EPI_PLAIN, t.as<double>(), nullptr, BjOp{}, nullptr,
+                              nullptr, nullptr, nullptr, 0, c->stream));
+        HIPCHK(c, launch_bj_apply(bj_op(M), n, t.as<double>(), sw.d, nullptr, nullptr, nullptr, vector_grid(n), nullptr, 0,
+                                  c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));   // t is freed on return
+    }
+    if (c->prof_on) prof_flush(c);
+    if (kind == VTK_PTR_HOST) {
+        HIPCHK(c, hipMemcpyAsync(w, sw.d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return VTK_OK;
+}
 
 int vtk_prec_kind_of(vtk_prec *M, int *kind) {
     if (!M || !kind) return VTK_ERR_ARG;

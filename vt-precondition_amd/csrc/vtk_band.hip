@@ -64,6 +64,17 @@ constexpr int BAND_PF = 12;        // j <= this: next line's update operands pre
 // (here and in the x update's) is the same fused chain, so step j forms p_j exactly as step j-1
 // did.  (k_dc_update keeps the unfused operations of the oracle's sequence.)
 template <int OPT> constexpr int band_wpe() { return (OPT & 2) ? 6 : 4; }
+// OPT bit 2 (XCDP, a runtime bit): the two parts of a line range on ONE XCD.  Each part updates
+// one v-halo row on either side, which lies in the other part's rows: read alone, that row drags
+// its whole 128-B line from HBM (the band step's PMC fetch is ~9 % over its algorithmic bytes at
+// j >= 9).  Workgroups are dealt to the XCDs round-robin (blockIdx mod 8), so blockIdx b and b + 8
+// share an XCD's L2: logical block (range, part) = (8 (b / 16) + b mod 8, (b / 8) mod 2).  The
+// logical index also names the workgroup's partial slot, so the dots' sums keep their bits.
+__device__ __forceinline__ int band_block(int opt, int H) {
+    const int b = blockIdx.x;
+    if (!(opt & 4) || H != 2 || (gridDim.x & 15) != 0) return b;
+    return (((b >> 4) << 3) + (b & 7)) * 2 + ((b >> 3) & 1);
+}
 __device__ __forceinline__ double band_msub(double acc, double a, double b) { return __builtin_fma(-a, b, acc); }
 __device__ __forceinline__ double band_madd(double acc, double a, double b) { return __builtin_fma(a, b, acc); }
 template <int WU, int J, int VMODE = 0, bool GH = true, int OPT = 0>
@@ -84,7 +95,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
     if (stopped(&a.st->stop_col, j)) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int L = a.L, X = a.X, H = a.H_parts, LP = L / H;
-    const int b = blockIdx.x, R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
+    const int b = band_block(a.opt, H), R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
     const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
     const int v = v0 - 8 + tid;
     const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
@@ -122,6 +133,8 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
     // software pipeline (J <= BAND_PF, as the registers allow): the next line's update
     // operands are loaded during this line's SpMV and dots.  (A partial prefetch of 4 basis rows
     // for larger J measured slower: 1234 vs 1254 it/s, spills)
+    // (round 6: the prefetch for every J -- spilling a few values past BAND_PF -- measured j13
+    // 758 -> 755, j16 880 -> 944, j18 989 -> 1087 us in process; not kept)
     constexpr bool PF = J <= BAND_PF;
     constexpr bool SPF = PF && CANON && (OPT & 1);
     // update operands of iteration it's line on the lane's row: V_k (k < j), w_{j-1} (j = 0: v_0)
@@ -964,7 +977,10 @@ __global__ __launch_bounds__(GR) __attribute__((amdgpu_waves_per_eu(GR == 512 &&
     __syncthreads();
     for (int gi = gb; gi < ge; ++gi) {
         const Ld cu = nx;
-        load(gi + 1, nx);
+        // the next group's operands; across ranks not past the range's last group: the interior
+        // launch runs while the comm stream writes the halo planes, which a group beyond its
+        // range would read (the value was never used, the read still raced the write)
+        load(HALO ? min(gi + 1, ge - 1) : gi + 1, nx);
         const int r = gi * GR + tid;
         const bool act = r < n;
         const int rc = act ? r : n - 1;

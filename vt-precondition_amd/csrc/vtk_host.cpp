@@ -97,6 +97,7 @@ const char *vtk_status_string(int s) {
         case VTK_ERR_NOMEM: return "out of memory";
         case VTK_ERR_STATE: return "invalid state";
         case VTK_ERR_NODEVICE: return "no HIP device (no CPU fallback)";
+        case VTK_ERR_PEER: return "a peer rank failed mid-solve";
         default: return "unknown status";
     }
 }

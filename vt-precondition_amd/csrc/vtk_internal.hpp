@@ -39,6 +39,11 @@ struct GmresState {
 // step): per-step coefficients produced by the scalar kernel for the update pass
 constexpr int DC_MAXJ = 32;          // restart <= 32 in this mode (4 waves x 8 vectors per lane)
 constexpr int DC_NQ = 2 * DC_MAXJ + 3;   // reduction slots: s[32] | z[32] | alpha beta gamma
+// across ranks the all-reduced payload carries one more slot, the failure vote (vtk_ctx::d_scal
+// [DC_VOTE]; [DC_VOTE + 1] holds this rank's own vote, nonzero once a launch of it failed)
+constexpr int DC_VOTE = DC_NQ;
+constexpr int DC_NQV = DC_NQ + 1;
+constexpr int PEER_FAILED = 2;           // GmresState::breakdown: the vote stopped the cycle
 struct DcCoef {
     double s[DC_MAXJ];        // re-orthogonalisation coefficients of the candidate p_j
     double e[DC_MAXJ + 1];    // projection of w on [V_j, v_j]
@@ -172,9 +177,10 @@ struct Tuning {
     int band_lsv = 1;         // solver launches read the line-separable values (else SELL values)
     int sell_canon = 1;       // ... and canonical rows' columns from the line index (no codes)
     int band_canon = 1;       // the band step reads no codes on canonical rows
-    int band_opt = 3;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
+    int band_opt = 7;         // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
                               // C3: SpMV operands prefetched j00 254 -> 217 us, + three workgroups per
-                              // CU for j <= BAND_J3: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms)
+                              // CU for j <= BAND_J3: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms;
+                              // bit 2, a line range's two parts on one XCD: 40.56 -> 40.30 ms, round 6)
     int lsv_ring = 2048;      // > 0: the line path's table SpMV with x staged through LDS, ~that many
                               // workgroups (in-process A/B, C3 line solve: 8.64 -> 8.26 ms; 167 -> 105 us)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
@@ -190,6 +196,8 @@ struct Tuning {
     int line_fuse = 1;        // line path (one rank, canonical rows): the SpMV inside the sweep kernel
     int cyc_ring = 512;       // > 0: cycle-start residual and DCGS2 step 0 through the x-line ring
                               // (k_lsv_ring_epi, ~that many workgroups; 2D line-separable rows)
+    int fail_step = -1;       // (test hook) >= 0: this rank's DCGS2 step of that index fails in the
+                              // first cycle as a refused launch would (the peer-failure vote, vtk_gmres)
 };
 }  // namespace vtk
 
@@ -204,6 +212,7 @@ struct vtk_ctx {
                                           // RCCL communicator (VTK_COMM_SOLO=1, testing)
     ncclComm_t comm = nullptr;            // RCCL (production transport)
     bool host_comm = false;               // host-staged hooks (vtk_comm_init_host)
+    bool comm_broken = false;             // an RCCL call failed: vtk_ctx_destroy aborts the communicator
     vtk_host_comm hops{};
     int orth = VTK_ORTH_AUTO;
     vtk::Tuning tune;                     // A/B switches (vtk_ctx_set_tuning), env at creation

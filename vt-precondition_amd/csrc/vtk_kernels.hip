@@ -2547,6 +2547,9 @@ __global__ __launch_bounds__(NT) void k_dc_finalize(const double *part, int cnt,
     else q = 2 * DC_MAXJ + (b - (with_w ? 2 * j : j));
     const double t = block_sum(strided_sum<GMAX / NT, NT>(part + (size_t)q * GMAX, cnt, threadIdx.x), red);
     if (threadIdx.x == 0) scal[q] = t;
+    // the rank's failure vote (DC_VOTE, set by the host when one of its launches failed) rides
+    // in the step's all-reduce: a nonzero sum stops every rank at this step (dc_scalar_body)
+    if (b == 0 && threadIdx.x == 0) scal[DC_VOTE] = scal[DC_VOTE + 1];
 }
 
 hipError_t launch_dc_finalize(const double *part, int cnt, int j, int with_w, double *scal,

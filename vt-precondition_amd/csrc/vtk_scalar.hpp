@@ -115,6 +115,17 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
     int *const flags = sl.flags;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (st->stop_col < j) return;
+    // across ranks (scal all-reduced): a rank voted failure in this step's all-reduce -- every
+    // rank stops the cycle here, at the same step, with no x update (vtk_gmres returns an error)
+    if (!part && scal[DC_VOTE] != 0.0) {
+        if (tid == 0) {
+            st->breakdown = PEER_FAILED;
+            st->stop_col = j - 1;
+            st->xup_tag = -1;
+            if (stop_map) __hip_atomic_store(stop_map, j - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     const int with_w = closing ? 0 : 1;
     const int nq = with_w ? 2 * j + 3 : j + 1;
     const int M1 = m + 1;

@@ -308,6 +308,22 @@ class CsrOperator:
     def dot(self, x):
         return self.matvec(x)
 
+    def precond_matvec(self, M, x):
+        """w = M^-1 (A x) through the launch the solver's split DCGS2 step uses for this operator
+        (SciPy: ``M.matvec(A @ x)``; vtk_precond_matvec).  M: a BlockJacobi / LineJacobi of this
+        operator, or None (w = A x)."""
+        vx = _Vec(x, self.n_local)
+        mh = M.handle if M is not None else None
+        if vx.kind == _abi.PTR_DEVICE:
+            import torch
+            w = torch.empty_like(vx.obj)
+            check(lib().vtk_precond_matvec(self._h, mh, vx.ptr, C.c_void_p(w.data_ptr()), vx.kind), self.ctx.handle)
+            self.ctx.synchronize()
+            return w
+        w = np.empty(self.n_local)
+        check(lib().vtk_precond_matvec(self._h, mh, vx.ptr, _np_ptr(w), vx.kind), self.ctx.handle)
+        return w
+
     def download(self):
         """(indptr, indices[global], data) of this rank's rows, as stored on the device."""
         ip = np.empty(self.n_local + 1, np.int32)

@@ -22,6 +22,7 @@ ERR_SINGULAR = -4
 ERR_NOMEM = -5
 ERR_STATE = -6
 ERR_NODEVICE = -7
+ERR_PEER = -8       # a peer rank failed mid-solve; this rank left the solve at the same step
 
 PTR_HOST = 0
 PTR_DEVICE = 1
@@ -103,6 +104,7 @@ PROTOTYPES = {
     "vtk_linejacobi_set_compact": (C.c_int, [P, C.c_int]),
     "vtk_linejacobi_get_compact": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vtk_prec_kind_of": (C.c_int, [P, C.POINTER(C.c_int)]),
+    "vtk_precond_matvec": (C.c_int, [P, P, P, P, C.c_int]),
     "vtk_gmres": (C.c_int, [P, P, P, P, C.c_double, C.c_double, C.c_int, C.c_int64, C.c_int,
                             C.POINTER(C.c_int), C.POINTER(Stats)]),
     "vtk_gmres_set_orth": (C.c_int, [P, C.c_int]),
@@ -113,7 +115,7 @@ PROTOTYPES = {
 }
 
 
-ABI_VERSION = 5   # include/vtkrylov.h VTK_ABI_VERSION
+ABI_VERSION = 6   # include/vtkrylov.h VTK_ABI_VERSION
 
 
 class BandGeometry(C.Structure):
