@@ -280,7 +280,9 @@ def test_band_step_variants(vk_lib, gpu, name):
     """The band step's launch variants (tunings band_opt: bit 0 the SpMV operands in the next-line
     prefetch, bit 1 three workgroups per CU for j <= 2 with their own grid): the same update,
     SpMV and BJ arithmetic; the dots' partials follow the grid, so the solves agree within the
-    DCGS2 bars and each variant is bit-identical from run to run."""
+    DCGS2 bars and each variant is bit-identical from run to run.  Bit 2 (a line range's two parts
+    on one XCD: the partial slots follow the logical index) and bit 3 (the LDS-DMA L2 prefetch for
+    J > 12) change no sum: bit-identical to the variant without them."""
     p, A = _op(vk_lib, gpu, name)
     M = vk_lib.block_jacobi(A, 8)
     b = twin.rhs(p.n)
@@ -293,5 +295,9 @@ def test_band_step_variants(vk_lib, gpu, name):
         assert np.array_equal(xa, xb) and sa.inner_iters == sb.inner_iters, opt
         assert abs(sa.inner_iters - sr.inner_iters) <= 1, opt
         assert np.linalg.norm(xa - xr) / np.linalg.norm(xr) < 1e-9, opt
+        for extra in (4, 8, 12):
+            with gpu.tuning(band_opt=opt | extra):
+                xc, ic, sc = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+            assert ic == 0 and np.array_equal(xc, xa) and sc.inner_iters == sa.inner_iters, (opt, extra)
     M.close()
     A.close()

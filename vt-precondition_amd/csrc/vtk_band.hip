@@ -77,6 +77,17 @@ __device__ __forceinline__ int band_block(int opt, int H) {
 }
 __device__ __forceinline__ double band_msub(double acc, double a, double b) { return __builtin_fma(-a, b, acc); }
 __device__ __forceinline__ double band_madd(double acc, double a, double b) { return __builtin_fma(a, b, acc); }
+// OPT bit 3 (L2PF): the global rows a later line iteration reads -- its update's basis and w rows, its
+// SpMV's D and m rows -- are touched ahead of time by LDS-DMA loads (global_load_lds_dword, one lane
+// per 128-B segment, into a scratch word nobody reads): no VGPR holds them, so the walk keeps more
+// bytes in flight than the register prefetch alone (two lines ahead with it, one without it, J >
+// BAND_PF).  The barriers then are bare s_barriers after lgkmcnt(0): __syncthreads' release fence
+// would wait for the DMA (vmcnt(0)) at every barrier.  Only LDS is shared inside the kernel, so
+// lgkmcnt(0) + s_barrier orders everything the barrier has to.
+template <int OPT> __device__ __forceinline__ void band_sync() {
+    if constexpr (OPT & 8) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else __syncthreads();
+}
 template <int WU, int J, int VMODE = 0, bool GH = true, int OPT = 0>
 __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe<OPT>()))) void k_band_step(BandK a) {
     constexpr int BAND_RS = BAND_T;
@@ -86,6 +97,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
     __shared__ double wbuf[BAND_LP];
     __shared__ double red[DC_NQ];
     __shared__ double cs[BAND_JV], ce[BAND_JV], cp[BAND_JV];
+    __shared__ int pf_sink[64];   // L2PF: the DMA's destination (never read)
     constexpr int j = J;
     if (__builtin_nontemporal_load(&a.st->xup_tag) == j) {   // the cycle's x update
         dc_xupdate_body<BAND_XUP_XB, true>(a.V, a.ld, j, __builtin_nontemporal_load(&a.st->stop_col), a.n, a.cf, a.x,
@@ -117,7 +129,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
         cp[k] = a.cf->e_prev[k];
     }
     const double rinv = a.cf->rinv, qc = a.cf->q, ej = a.cf->e[j], qp = a.cf->q_prev;
-    __syncthreads();
+    band_sync<OPT>();
     double vreg[J + 1];
     double acc[BAND_IT][3];
 #pragma unroll
@@ -236,10 +248,44 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
         }
     };
     auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
+    // L2PF: touch the rows iteration itp reads (its line's rows v0 - 1 .. v0 + LP of the J basis
+    // vectors, w_j and w_{j-1} (v_0 at j = 0); D and m of its SpMV line), 128-B segments, the
+    // rows spread over the waves.  Ghost lines (a neighbour rank's) come from the ghost buffer: skipped
+    constexpr int PF_ROWS = J + 2 + (CANON ? 2 : 0);
+    auto l2_prefetch = [&](int itp) {
+        if constexpr ((OPT & 8) != 0) {
+            if (itp > nl + 1) return;
+            int kind;
+            const int y = line_of(itp, kind);
+            const bool ghostl = GH && a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1));
+            const int xs = xa - 2 + itp;   // its SpMV line (owned when itp >= 2)
+            const int vlo = v0 > 0 ? v0 - 1 : 0, vhi = v0 + LP < L ? v0 + LP + 1 : L;
+            for (int r = wv; r < PF_ROWS; r += BAND_W) {   // wave-uniform
+                const double *vec;
+                int64_t r0, r1;
+                if (r < J + 2) {
+                    if (ghostl) continue;
+                    vec = r < J ? a.V + (size_t)r * a.ld : (r == J ? a.w_in : (j == 0 ? a.V : a.w_prev));
+                    r0 = (int64_t)y * L + vlo;
+                    r1 = (int64_t)y * L + vhi;
+                } else {
+                    if (itp < 2) continue;
+                    vec = r == J + 2 ? a.lsv : a.mtri;
+                    r0 = (int64_t)xs * L + v0;
+                    r1 = r0 + LP;
+                }
+                const int64_t s0 = r0 >> 4, ns = ((r1 - 1) >> 4) - s0 + 1;   // 16 doubles = 128 B
+                if (lane < ns)
+                    __builtin_amdgcn_global_load_lds(vec + ((s0 + lane) << 4), (__attribute__((address_space(3))) void *)pf_sink,
+                                                     4, 0, 0);
+            }
+        }
+    };
     // iteration it updates line y = xa - 1 + it and, from it = 2 on, runs the SpMV and dots of
     // line y - 1
     Ld nx;
     if constexpr (PF) load(0, nx);
+    l2_prefetch(PF ? 1 : 0);   // (L2PF only)
     for (int it = 0; it <= nl + 1; ++it) {
         const int y = xa - 1 + it, x = y - 1;
         const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
@@ -284,8 +330,9 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             if constexpr (PF) {
                 if (it <= nl) load(it + 1, nx);
             }
+            l2_prefetch(PF ? it + 2 : it + 1);   // (L2PF only)
         }
-        __syncthreads();
+        band_sync<OPT>();
         if (work) {
             // 2. w = M^-1 A p_{j+1} on the part's rows of line x, gathers from the ring
             double sacc = 0.0, sub = 0.0, sup = 0.0;
@@ -389,7 +436,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                 st_wt(a.w_out + row, z);
                 wbuf[tid - 8] = z;
             }
-            __syncthreads();
+            band_sync<OPT>();
             // 3. dots of the part's rows of line x: wave wv owns items wv, wv + 7, wv + 14 (item
             //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows.  Items
             //    outer: each item's loop streams one basis row against p and w (rows outer with
@@ -416,7 +463,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                     }
                 }
             }
-            __syncthreads();
+            band_sync<OPT>();
         }
         if (it >= 1 && it <= nl) stage(vbuf);   // line y is owned: its basis rows for the dots one line on
     }
@@ -450,6 +497,12 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
 // variant bits of a.opt; WPC3 only where the LDS of three workgroups fits (J <= BAND_J3)
 template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipStream_t s) {
     const dim3 g(grid), blk(BAND_T);
+    // L2PF where the registers hold no next line (J > BAND_PF).  In-process A/B (C3, round 6): j13-j17
+    // 745-925 -> 709-875 us, j18 991 -> 970; with the register prefetch (J <= 12, two lines ahead)
+    // it cost 11-35 us per launch
+    if constexpr (J > BAND_PF) {
+        if (a.opt & 8) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 9>), g, blk, 0, s, a); return; }
+    }
     if constexpr (J <= BAND_J3) {
         if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 3>), g, blk, 0, s, a); return; }
         if ((a.opt & 3) == 2) { hipLaunchKernelGGL((k_band_step<5, J, 2, false, 2>), g, blk, 0, s, a); return; }
