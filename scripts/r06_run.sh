@@ -12,7 +12,7 @@ band) run t_band 600 $T tests/test_gpu_band.py ;;
 tests) run t_sel 900 $T ${TESTS} ;;
 gpu) run t_gpu 1100 $T tests -m gpu ;;
 smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-ab) run ab_${AB_ENV} 600 python tools/ab_env.py --env "$AB_ENV" --values "${AB_VALUES:-1,0}" --rounds "${AB_ROUNDS:-4}" --config "${AB_CFG:-C3}" --set "${AB_SET:-}" --perj ;;
+ab) run ab_${AB_ENV}${AB_TAG:-} 600 python tools/ab_env.py --env "$AB_ENV" --values "${AB_VALUES:-1,0}" --rounds "${AB_ROUNDS:-4}" --config "${AB_CFG:-C3}" --set "${AB_SET:-}" --perj ${AB_EXTRA:-} ;;
 bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
 slabs) for cp in C3:8 C3:4 C3:2 C4:8; do c=${cp%%:*}; p=${cp##*:}
          run slab_${c}_$p 300 python bench.py --config $c --slab $p --comm-solo --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 2
@@ -34,6 +34,13 @@ final4) P="python bench.py --config C4 --steps 1 --warmup 1 --no-cpu-baseline --
 sq) run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py ${SQ_ARGS:-} --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
 line) run bench_line 300 python bench.py --prec line --steps 5 --warmup 1 --no-cpu-baseline
       run prof_line 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_line -o run --output-format csv -- python bench.py --prec line --steps 3 --warmup 1 --no-cpu-baseline ;;
+linepmc) P="python bench.py --prec line --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5"
+         run prof_line 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_line -o run --output-format csv -- $P
+         run pmcf_line 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_line -o run --output-format csv -- $P
+         run pmcw_line 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_line -o run --output-format csv -- $P ;;
+gh2) for v in ${GH_VALUES:-0 15 0 15}; do
+       VTK_BAND_OPT=$v run gh2_$v 400 python bench.py --gpus 2 --comm host --config ${GH_CFG:-C3} --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 2
+       grep '^{' gpurun_out/gh2_$v.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('band_opt', $v, round(d['value'],1), 'it/s', d.get('kernels',{}).get('band_step'))" >> gpurun_out/gh2.txt; done ;;
 membench) run build_mb 200 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/membench_layout tools/membench_layout.hip
           run membench_layout 300 /tmp/membench_layout ;;
 *) echo "unknown stage $st"; exit 2 ;;

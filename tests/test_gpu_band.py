@@ -299,5 +299,13 @@ def test_band_step_variants(vk_lib, gpu, name):
             with gpu.tuning(band_opt=opt | extra):
                 xc, ic, sc = _solve(vk_lib, gpu, A, M, b, True, restart=20)
             assert ic == 0 and np.array_equal(xc, xa) and sc.inner_iters == sa.inner_iters, (opt, extra)
+        # bit 4: odd line ranges walk backwards (their dots sum the lines in reverse order): the
+        # DCGS2 bars against the reference, bit-identical from run to run
+        with gpu.tuning(band_opt=opt | 28):
+            xd, idd, sd = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+            xe, _, se = _solve(vk_lib, gpu, A, M, b, True, restart=20)
+        assert idd == 0 and sd.band == 1 and np.array_equal(xd, xe) and sd.inner_iters == se.inner_iters, opt
+        assert abs(sd.inner_iters - sr.inner_iters) <= 1, opt
+        assert np.linalg.norm(xd - xr) / np.linalg.norm(xr) < 1e-9, opt
     M.close()
     A.close()

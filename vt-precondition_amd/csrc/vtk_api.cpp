@@ -1238,10 +1238,10 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // line-separable values in the band step (tuning band_lsv 0: the SELL values)
     const bool band_lsv = band && s.A->d_lsv && c->tune.band_lsv;
     const bool band_canon = c->tune.band_canon != 0;       // 0: read the codes anyway (A/B)
-    // the band step's variant bits exist for the one-rank instantiation (line-separable values,
-    // canonical rows, no ghost lines; launch_band_one_rank): every other launch, and the partial
-    // count its successor reads, takes the base grid
-    const int band_opt = band_lsv && s.A->lsv_canon && band_canon && !s.ghost ? c->tune.band_opt : 0;
+    // the band step's variant bits exist for the line-separable, canonical-row instantiations (one
+    // rank: launch_band_one_rank; across ranks with ghost lines: launch_band_ghost, round 6): every
+    // other launch, and the partial count its successor reads, takes the base grid
+    const int band_opt = band_lsv && s.A->lsv_canon && band_canon ? c->tune.band_opt : 0;
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)
     const double b_band = band_lsv ? (s.A->lsv_canon && band_canon

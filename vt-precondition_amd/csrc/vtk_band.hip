@@ -138,10 +138,24 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
     // kind 1 / 2, recomputed, nothing stored)
     const int nl = xb - xa;
     const int xhm = xa == 0 ? X - 1 : xa - 1, xhp = xb == X ? 0 : xb;   // the x-halo lines (mod X)
+    // opt bit 4 (ALT): odd line ranges walk their lines backwards, so that the two workgroups on
+    // either side of every range boundary read the boundary's two lines (each one's own line and
+    // the other's x-halo line) at the same time, at the start or at the end of both walks: the
+    // second read finds the line in the Infinity Cache instead of HBM.  (The dots then sum an
+    // odd range's lines in reverse order: not the bits of the forward walk, within the DCGS2 bars.)
+    const bool rev = (a.opt & 16) && (rb & 1);
+    // kind 1 / 2: the left / right x-halo line (a forward walk's first / last iteration)
     auto line_of = [&](int it, int &kind) {
+        if (rev) {
+            kind = it == 0 ? 2 : (it == nl + 1 ? 1 : 0);
+            return it == 0 ? xhp : (it == nl + 1 ? xhm : xb - it);
+        }
         kind = it == 0 ? 1 : (it == nl + 1 ? 2 : 0);
         return it == 0 ? xhm : (it == nl + 1 ? xhp : xa - 1 + it);
     };
+    // the owned line whose SpMV and dots iteration it (>= 2) runs: the line updated one iteration
+    // before, whose x-neighbours are both in the ring now
+    auto spmv_line = [&](int it) { return rev ? xb + 1 - it : xa - 2 + it; };
     // software pipeline (J <= BAND_PF, as the registers allow): the next line's update
     // operands are loaded during this line's SpMV and dots.  (A partial prefetch of 4 basis rows
     // for larger J measured slower: 1234 vs 1254 it/s, spills)
@@ -166,7 +180,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             o.mrow = 1.0;
             o.tv0 = o.tv1 = 0.0;
             if (it >= 2) {
-                const int xs = xa - 2 + it;
+                const int xs = spmv_line(it);
                 const int64_t rs = (int64_t)xs * L + (own ? v : v0);
                 if (own) {
                     o.drow = __builtin_nontemporal_load(a.lsv + rs);
@@ -258,8 +272,11 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             int kind;
             const int y = line_of(itp, kind);
             const bool ghostl = GH && a.ghost && ((kind == 1 && rb == 0) || (kind == 2 && rb == R - 1));
-            const int xs = xa - 2 + itp;   // its SpMV line (owned when itp >= 2)
+            const int xs = spmv_line(itp);   // its SpMV line (owned when itp >= 2)
             const int vlo = v0 > 0 ? v0 - 1 : 0, vhi = v0 + LP < L ? v0 + LP + 1 : L;
+            // (round 6: capping the prefetch at 10 basis rows -- a line's J + 4 rows of ~3.3 KB per
+            // workgroup, 64 workgroups per XCD, overflow the 4 MB L2 past ~14 rows: PMC fetch 1.07x at
+            // j = 13, 1.19x at j = 18 -- made j13-j18 11-33 us slower in process: not kept)
             for (int r = wv; r < PF_ROWS; r += BAND_W) {   // wave-uniform
                 const double *vec;
                 int64_t r0, r1;
@@ -281,13 +298,15 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             }
         }
     };
-    // iteration it updates line y = xa - 1 + it and, from it = 2 on, runs the SpMV and dots of
-    // line y - 1
+    // iteration it updates line y = xa - 1 + it (ALT, odd ranges: xb - it) and, from it = 2 on,
+    // runs the SpMV and dots of line y - 1 (ALT, odd ranges: y + 1)
     Ld nx;
     if constexpr (PF) load(0, nx);
     l2_prefetch(PF ? 1 : 0);   // (L2PF only)
     for (int it = 0; it <= nl + 1; ++it) {
-        const int y = xa - 1 + it, x = y - 1;
+        // y: the updated line's logical index (xa - 1 .. xb, unwrapped: its ring slot), x: the
+        // SpMV line (owned when it >= 2)
+        const int y = rev ? xb - it : xa - 1 + it, x = spmv_line(it);
         const bool work = it >= 2;   // line x = y - 1 is owned: SpMV + dots
         const int64_t lrow = (int64_t)(work ? x : xa) * L;
         const int64_t row = lrow + (own ? v : v0);
@@ -511,6 +530,25 @@ template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipS
     else hipLaunchKernelGGL((k_band_step<5, J, 2, false>), g, blk, 0, s, a);
 }
 
+// across ranks (ghost lines, canonical rows, line-separable values): the same variants as one rank
+// -- until round 6 the distributed band step ran OPT 0 only (no SpMV operands in the prefetch, no
+// third workgroup per CU at low j, no LDS-DMA prefetch at high j), which the one-rank slab
+// projections (--comm-solo: no ghost lines) did not see.  The ghost lines' update operands come from
+// the ghost buffer in load(); the DMA prefetch skips them (l2_prefetch's ghostl)
+template <int J> static void launch_band_ghost(const BandK &a, int grid, hipStream_t s) {
+    const dim3 g(grid), blk(BAND_T);
+    if constexpr (J > BAND_PF) {
+        if (a.opt & 8) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 9>), g, blk, 0, s, a); return; }
+    }
+    if constexpr (J <= BAND_J3) {
+        if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 3>), g, blk, 0, s, a); return; }
+    }
+    if constexpr (J > BAND_J3 && J <= BAND_PF) {
+        if (a.opt & 1) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 1>), g, blk, 0, s, a); return; }
+    }
+    hipLaunchKernelGGL((k_band_step<5, J, 2>), g, blk, 0, s, a);
+}
+
 hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
     if (wu != 5 || a.H_parts < 1 || a.L % a.H_parts != 0 || a.L / a.H_parts > BAND_LP || (a.L / a.H_parts) % 8 != 0 ||
         a.j + 1 > BAND_JV || grid < a.H_parts || grid > GMAX || grid % a.H_parts != 0 || grid / a.H_parts > a.X ||
@@ -520,7 +558,7 @@ hipError_t launch_band_step(const BandK &a, int grid, int wu, hipStream_t s) {
 #define VTK_BAND_J(J_)                                                                                           \
     case J_:                                                                                                     \
         if (a.lsv && a.canon && !a.ghost) launch_band_one_rank<J_>(a, grid, s); \
-        else if (a.lsv && a.canon) hipLaunchKernelGGL((k_band_step<5, J_, 2>), dim3(grid), dim3(BAND_T), 0, s, a); \
+        else if (a.lsv && a.canon) launch_band_ghost<J_>(a, grid, s); \
         else if (a.lsv) hipLaunchKernelGGL((k_band_step<5, J_, 1>), dim3(grid), dim3(BAND_T), 0, s, a); \
         else hipLaunchKernelGGL((k_band_step<5, J_>), dim3(grid), dim3(BAND_T), 0, s, a); \
         break;

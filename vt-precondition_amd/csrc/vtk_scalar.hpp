@@ -106,15 +106,22 @@ __device__ __forceinline__ void dc_sum_partials(double *q, const double *part, i
 //    at once (Givens, stop test) when its estimate is numerically safe — no cancellation in
 //    nu (nu > 1e-3 ||Bv||) and presid not within 1e-8 of ptol — or it is the cycle's last
 //    column; otherwise it is finalised exactly by step j+1.
-template <bool SC1, int QW>
+// TR: phase marks for tools/probe_scalar.hip (the product's ScalarNoTrace marks nothing)
+struct ScalarNoTrace {
+    __device__ __forceinline__ void mark(int) const {}
+};
+template <bool SC1, int QW, class TR = ScalarNoTrace>
 __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *part, int cnt, const double *scal,
                                                int j, int m, int closing, double *Hraw, double *H, double *S,
-                                               double *giv, DcCoef *cf, GmresState *st, int *stop_map) {
+                                               double *giv, DcCoef *cf, GmresState *st, int *stop_map,
+                                               TR tr = TR{}) {
     double *const q = sl.q, *const hr_s = sl.hr_s, *const giv_s = sl.giv_s, *const S_s = sl.S_s;
     double *const hc_s = sl.hc_s, *const hj = sl.hj, *const e_s = sl.e_s, *const sc = sl.sc;
     int *const flags = sl.flags;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    tr.mark(0);
     if (st->stop_col < j) return;
+    tr.mark(1);
     // across ranks (scal all-reduced): a rank voted failure in this step's all-reduce -- every
     // rank stops the cycle here, at the same step, with no x update (vtk_gmres returns an error)
     if (!part && scal[DC_VOTE] != 0.0) {
@@ -156,6 +163,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
         flags[1] = 0;
     }
     __syncthreads();
+    tr.mark(2);
     const double *sv = q, *zv = q + DC_MAXJ;
     const double alpha = q[2 * DC_MAXJ], beta = q[2 * DC_MAXJ + 1], gamma = q[2 * DC_MAXJ + 2];
     const double ptol = sc[0];
@@ -226,6 +234,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
         }
     }
     __syncthreads();
+    tr.mark(3);
     // phase B2 (lane 0): breakdown test, Givens and stop test of column j-1
     if (tid == 0) {
         if (fin_prev) {
@@ -238,6 +247,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
         if (closing) flags[1] = 1;
     }
     __syncthreads();
+    tr.mark(4);
     if (flags[1]) return;
     // phase C (lanes k <= j): tentative column j, c'_k = (e_k - (H_j s)_k) / r, with the raw
     // columns i < j final; row k of column i is nonzero for i >= k-1
@@ -256,6 +266,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
         if (k < j) cf->s[k] = sv[k];
     }
     __syncthreads();
+    tr.mark(5);
     if (wv != 0) return;
     const double ek = lane <= j ? e_s[lane] : 0.0;
     const double ee = wave_allsum(ek * ek);
@@ -272,6 +283,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
     cf->q_prev = cf->q;
     cf->q = 1.0 / (r * nu);
     cf->committed[j] = 0;
+    tr.mark(6);
     if (!safe) return;
     // trial rotation of the tentative column (only the last rotated entry is needed)
     double a0 = hj[0];
@@ -281,6 +293,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
     const double pres_t = __builtin_fabs(-sg * S_s[j]);
     const bool last = j == m - 1;
     if (!(last || pres_t <= ptol * (1.0 - 1e-8))) return;   // above or ambiguous: finalise exactly
+    tr.mark(7);
     for (int k = 0; k <= j; ++k) hc_s[k] = hj[k];
     hc_s[j + 1] = nu;
     cf->committed[j] = 1;
@@ -289,6 +302,7 @@ __device__ __forceinline__ void dc_scalar_body(DcScalarLds &sl, const double *pa
         st->xup_tag = j;
         if (stop_map) __hip_atomic_store(stop_map, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    tr.mark(8);
 }
 
 }  // namespace vtk
