@@ -50,7 +50,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&giv, sizeof(double) * 2 * M1));
     CK(hipMalloc(&cf, sizeof(DcCoef)));
     CK(hipMalloc(&st, sizeof(GmresState)));
-    CK(hipMalloc(&t, sizeof(long long) * 16));
+    CK(hipMalloc(&t, sizeof(long long) * 32));
     // partials: s_k small, z_k small, alpha ~ 1, beta, gamma ~ 1 (r, nu well away from cancellation)
     std::vector<double> hp((size_t)DC_NQ * GMAX, 0.0);
     for (int q = 0; q < DC_NQ; ++q)

@@ -177,11 +177,13 @@ struct Tuning {
     int band_lsv = 1;         // solver launches read the line-separable values (else SELL values)
     int sell_canon = 1;       // ... and canonical rows' columns from the line index (no codes)
     int band_canon = 1;       // the band step reads no codes on canonical rows
-    int band_opt = 15;        // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
+    int band_opt = 31;        // band step variant bits (vtk_band.hip k_band_step OPT; in-process A/B
                               // C3: SpMV operands prefetched j00 254 -> 217 us, + three workgroups per
                               // CU for j <= BAND_J3: j00 190, j01 283 -> 246 us; solve 42.66 -> 42.31 ms;
                               // round 6: bit 2, a line range's two parts on one XCD: 40.56 -> 40.30 ms;
-                              // bit 3, LDS-DMA L2 prefetch for J > BAND_PF: j13-j18 -21..-50 us each)
+                              // bit 3, LDS-DMA L2 prefetch for J > BAND_PF: j13-j18 -21..-50 us each;
+                              // bit 4, odd line ranges walk backwards: 39.98 -> 39.81 ms, C3/8 slab
+                              // 6.652 vs 6.676 ms (neutral).  Since round 6 also across ranks)
     int lsv_ring = 2048;      // > 0: the line path's table SpMV with x staged through LDS, ~that many
                               // workgroups (in-process A/B, C3 line solve: 8.64 -> 8.26 ms; 167 -> 105 us)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
