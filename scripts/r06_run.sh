@@ -12,7 +12,7 @@ band) run t_band 600 $T tests/test_gpu_band.py ;;
 tests) run t_sel 900 $T ${TESTS} ;;
 gpu) run t_gpu 1100 $T tests -m gpu ;;
 smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-ab) run ab_${AB_ENV}${AB_TAG:-} 600 python tools/ab_env.py --env "$AB_ENV" --values "${AB_VALUES:-1,0}" --rounds "${AB_ROUNDS:-4}" --config "${AB_CFG:-C3}" --set "${AB_SET:-}" --perj ${AB_EXTRA:-} ;;
+ab) run ab_${AB_ENV}${AB_TAG:-} 600 python tools/ab_env.py --env "$AB_ENV" --values "${AB_VALUES:-1,0}" --rounds "${AB_ROUNDS:-4}" --config "${AB_CFG:-C3}" --set "${AB_SET:-}" --perj ${AB_EXTRA:-} ${AB_MAXITER:+--maxiter $AB_MAXITER} ;;
 bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
 slabs) for cp in C3:8 C3:4 C3:2 C4:8; do c=${cp%%:*}; p=${cp##*:}
          run slab_${c}_$p 300 python bench.py --config $c --slab $p --comm-solo --steps 5 --warmup 1 --no-cpu-baseline --spmv-reps 2

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--comm-solo", action="store_true", help="the distributed code path on one rank (bench.py --comm-solo)")
     ap.add_argument("--perj", action="store_true", help="also one profiled solve per value: band step us per j")
     ap.add_argument("--set", default="", help="fixed tuning for every value, e.g. band_opt=1,lsv_ring=0")
+    ap.add_argument("--maxiter", type=int, default=None,
+                    help="restart cycles per solve (timing-only variants whose numerics do not converge)")
     a = ap.parse_args()
     import vtkrylov as vk
     from oracle import twin
@@ -60,7 +62,7 @@ def main():
         for v in (vals if r % 2 == 0 else vals[::-1]):
             ctx.set_tuning(key, int(v))
             t = time.perf_counter()
-            _, info = vk.gmres(A, b, rtol=a.rtol, M=M)
+            _, info = vk.gmres(A, b, rtol=a.rtol, M=M, maxiter=a.maxiter)
             dt = (time.perf_counter() - t) * 1e3
             st = vk.last_stats()
             iters[v] = (st.inner_iters, st.band, info)
@@ -72,7 +74,7 @@ def main():
         for v in vals:
             ctx.set_tuning(key, int(v))
             ctx.profile(True)
-            vk.gmres(A, b, rtol=a.rtol, M=M)
+            vk.gmres(A, b, rtol=a.rtol, M=M, maxiter=a.maxiter)
             pr = ctx.profile_read()
             ctx.profile(False)
             perj[v] = {k: round(e["avg_us"], 1) for k, e in sorted(pr.items())
