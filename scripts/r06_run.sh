@@ -41,6 +41,10 @@ linepmc) P="python bench.py --prec line --steps 1 --warmup 1 --no-cpu-baseline -
 gh2) for v in ${GH_VALUES:-0 15 0 15}; do
        VTK_BAND_OPT=$v run gh2_$v 400 python bench.py --gpus 2 --comm host --config ${GH_CFG:-C3} --steps 3 --warmup 1 --no-cpu-baseline --spmv-reps 2
        grep '^{' gpurun_out/gh2_$v.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('band_opt', $v, round(d['value'],1), 'it/s', d.get('kernels',{}).get('band_step'))" >> gpurun_out/gh2.txt; done ;;
+cfgs) run bench_c1 300 python bench.py --config C1 --steps 5 --warmup 1
+      run bench_c2 300 python bench.py --config C2 --steps 5 --warmup 1
+      run prof_c2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python bench.py --config C2 --steps 1 --warmup 1 --no-cpu-baseline --spmv-reps 5 ;;
+c3x) for r in 1 2; do run bench_c3_$r 300 python bench.py --no-cpu-baseline; done ;;
 membench) run build_mb 200 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/membench_layout tools/membench_layout.hip
           run membench_layout 300 /tmp/membench_layout ;;
 *) echo "unknown stage $st"; exit 2 ;;

@@ -35,6 +35,16 @@ __global__ __launch_bounds__(1024) void k_probe(const double *part, int cnt, con
     dc_scalar_body<false, 3, Marks>(sl, part, cnt, scal, j, m, 0, Hraw, H, S, giv, cf, st, nullptr, Marks{t});
 }
 
+// launch geometry variants of the plain scalar kernel (no marks): NTH threads, QW quantities per
+// wave per round -- back-to-back launch time is what the solver's chain pays
+template <int NTH, int QW>
+__global__ __launch_bounds__(NTH) void k_geo(const double *part, int cnt, const double *scal, int j, int m,
+                                             double *Hraw, double *H, double *S, double *giv, DcCoef *cf,
+                                             GmresState *st) {
+    __shared__ DcScalarLds sl;
+    dc_scalar_body<false, QW>(sl, part, cnt, scal, j, m, 0, Hraw, H, S, giv, cf, st, nullptr);
+}
+
 int main(int argc, char **argv) {
     const int cnt = argc > 1 ? std::atoi(argv[1]) : 512, reps = argc > 2 ? std::atoi(argv[2]) : 50;
     const int m = 20, M1 = m + 1;
@@ -115,6 +125,31 @@ int main(int argc, char **argv) {
             std::sort(ph[0].begin(), ph[0].end());
             std::printf(" | tot %6.2f | 2 launches %6.2f us\n", ph[0][ph[0].size() / 2], 1000.f * ms_sum / reps);
         }
+    }
+    // back-to-back launches (state reset once per batch; the path taken stays the uncommitted
+    // one only for the first launch of a batch -- the later ones find column j-1 committed)
+    std::printf("back-to-back: us per launch (100 launches), j: 1024x3  256x3  256x11  64x22\n");
+    for (int j = 0; j < m; j += 3) {
+        float us[4];
+        for (int v = 0; v < 4; ++v) {
+            hc.committed[j > 0 ? j - 1 : 0] = 0;
+            CK(hipMemcpy(cf, &hc, sizeof hc, hipMemcpyHostToDevice));
+            CK(hipMemcpy(st, &hs, sizeof hs, hipMemcpyHostToDevice));
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0));
+            for (int r = 0; r < 100; ++r) {
+                if (v == 0) hipLaunchKernelGGL((k_geo<1024, 3>), dim3(1), dim3(1024), 0, 0, part, cnt, scal, j, m, Hraw, H, S, giv, cf, st);
+                if (v == 1) hipLaunchKernelGGL((k_geo<256, 3>), dim3(1), dim3(256), 0, 0, part, cnt, scal, j, m, Hraw, H, S, giv, cf, st);
+                if (v == 2) hipLaunchKernelGGL((k_geo<256, 11>), dim3(1), dim3(256), 0, 0, part, cnt, scal, j, m, Hraw, H, S, giv, cf, st);
+                if (v == 3) hipLaunchKernelGGL((k_geo<64, 22>), dim3(1), dim3(64), 0, 0, part, cnt, scal, j, m, Hraw, H, S, giv, cf, st);
+            }
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            us[v] = 10.f * ms;
+        }
+        std::printf("j %2d: %7.2f %7.2f %7.2f %7.2f\n", j, us[0], us[1], us[2], us[3]);
     }
     return 0;
 }
