@@ -1548,18 +1548,23 @@ __global__ __launch_bounds__(NT) void k_line_apply(LineOp L, const double *r, do
 
 // Line path, one rank, canonical line-separable rows: the table SpMV y = A p
 // formed inside the sweep kernel -- the lane's column of p along its segment, one line either
-// side, in registers; p at v -+ 1 from the neighbouring lanes (DPP wave shifts; a wave covers 62 positions plus
-// one halo column each side) -- then k_line_apply's sweeps and dots on it (COMPACT, DCD).  y is
-// neither written nor read back (two vectors less per step) and p is read once for the SpMV and
-// the dots.  The SpMV's products and their order are k_lsv_ring's (canonical row order), the
-// sweeps k_line_apply's: w is bit-identical to the two-kernel form; the dots' partials follow the
-// 62-lane blocks (another fixed order: the DCGS2 bars).
+// side, in registers; p at v -+ 1 from the neighbouring lanes (DPP wave shifts; a wave covers 64
+// positions, 128-B aligned rows, and the two columns just outside them arrive in LDS by LDS-DMA:
+// no VGPR holds them -- round 6; the 62-position waves with a halo lane either side read
+// misaligned 512-B rows, five cache lines for four, PMC 1.15x) -- then k_line_apply's sweeps and
+// dots on it (COMPACT, DCD).  y is neither written nor read back (two vectors less per step) and
+// p is read once for the SpMV and the dots.  The SpMV's products and their order are
+// k_lsv_ring's (canonical row order), the sweeps k_line_apply's: w is bit-identical to the
+// two-kernel form; the dots' partials follow the 64-lane blocks (another fixed order: the DCGS2
+// bars).
 template <int LMAX>
 __global__ __launch_bounds__(NT) void k_line_spmv_dc(LineOp L, const double *__restrict__ lsv,
                                                      const double *__restrict__ p, double *__restrict__ w, int nb,
                                                      const int *stop_col, int col, LineDc dc) {
     constexpr int NQW = 2 * DC_MAXJ + 3;
+    constexpr int HW = 4 * LMAX <= 64 ? 1 : 2;   // LDS-DMA instructions for the halo columns
     __shared__ double stage[(NT / 64) * NQW];
+    __shared__ double halo[NT / 64][32 * HW];    // per wave: [line u][left, right] of the 64 columns
     if (stopped(stop_col, col)) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int n = (int)L.n, Lb = (int)L.stride, X = n / Lb, seg = (int)L.seg;
@@ -1569,12 +1574,23 @@ __global__ __launch_bounds__(NT) void k_line_spmv_dc(LineOp L, const double *__r
     for (int64_t t = (int64_t)blockIdx.x * (NT / 64) + wv; t < nitems; t += (int64_t)gridDim.x * (NT / 64)) {
         const int sg = (int)(t / nb), jw = (int)(t - (int64_t)sg * nb);
         const int xb = sg * seg, len = min(seg, X - xb);
-        const int vv = jw * 62 + lane - 1;   // lanes 0 and 63: the halo columns v - 1, v + 1
-        const bool inl = vv >= 0 && vv < Lb;
-        const bool use = inl && lane >= 1 && lane <= 62;
-        const int v = inl ? vv : 0;
+        const int v0 = jw * 64, vv = v0 + lane;
+        const bool use = vv < Lb;
+        const int v = use ? vv : 0;
         const double aj = use ? L.ac[v] : 0.0, cj = use ? L.ac[L.jn + v] : 0.0;
         const double tx0 = lsv[n + v], tx1 = lsv[n + Lb + v];
+        // the columns v0 - 1 and v0 + 64 of lines xb .. xb + len - 1 (the v -+ 1 neighbours of the
+        // wave's first and last lane), one dword per lane straight into LDS; a column off the line
+        // (v0 = 0, or v0 + 64 >= Lb: its term is skipped) reads the wave's own column instead
+#pragma unroll
+        for (int i = 0; i < HW; ++i) {
+            const int d = 64 * i + lane, u = d >> 2, side = (d >> 1) & 1, half = d & 1;
+            const int x = xb + min(u, len - 1);
+            int vc = side ? v0 + 64 : v0 - 1;
+            vc = vc < 0 || vc >= Lb ? v0 : vc;
+            const char *src = reinterpret_cast<const char *>(p + (x * Lb + vc)) + 4 * half;
+            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)&halo[wv][32 * i], 4, 0, 0);
+        }
         // p on the column: lines xb - 1 .. xb + len (periodic in x)
         double pc[LMAX + 2];
 #pragma unroll
@@ -1583,6 +1599,11 @@ __global__ __launch_bounds__(NT) void k_line_spmv_dc(LineOp L, const double *__r
             x = x < 0 ? x + X : (x >= X ? x - X : x);
             pc[u] = ld_nt<8>(p + (x * Lb + v));
         }
+        // every column load is in flight before the first wait (unfenced, the scheduler hoists the
+        // first line's DPP shifts above the later loads: one memory latency per item); the halo
+        // columns have landed once at most the column loads are outstanding (in order)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LMAX + 2) : "memory");
         double e[LMAX], gg[LMAX];
         double dp = 0.0, mp = 0.0;
         bool pok = false;
@@ -1597,8 +1618,11 @@ __global__ __launch_bounds__(NT) void k_line_spmv_dc(LineOp L, const double *__r
             const double drow = ld_nt<8>(lsv + (x * Lb + v));
             const double tv0 = lsv[n + 2 * Lb + x], tv1 = lsv[n + 2 * Lb + X + x];
             const double c0 = pc[u + 1];
-            // v -+ 1: the neighbouring lanes' values by DPP wave shifts (wave_shr:1 / wave_shl:1)
-            const double pm = dpp_mov<0x138>(c0), pq = dpp_mov<0x130>(c0);
+            // v -+ 1: the neighbouring lanes' values by DPP wave shifts (wave_shr:1 / wave_shl:1),
+            // the first and last lane's from the halo columns in LDS
+            const double hm = halo[wv][2 * u], hq = halo[wv][2 * u + 1];
+            const double sm = dpp_mov<0x138>(c0), sq = dpp_mov<0x130>(c0);
+            const double pm = lane == 0 ? hm : sm, pq = lane == 63 ? hq : sq;
             const double t0 = tx0 * pc[u], t4 = tx1 * pc[u + 2], t2 = drow * c0, t1 = tv0 * pm, t3 = tv1 * pq;
             const bool h1 = v > 0, h3 = v < Lb - 1;
             double sa = 0.0;
@@ -1702,7 +1726,7 @@ hipError_t launch_line_spmv_dc(const LineOp &L, const double *lsv, const double 
         L.i_lo != 0 || L.i_hi != X - 1 || L.seg <= 0 || L.seg > 32 || j < 0 || j > DC_MAXJ || grid < 1 ||
         grid > GMAX || L.n > INT32_MAX / 2 || !lsv || !p || !part)
         return hipErrorInvalidValue;
-    const int nb = (int)((Lb + 61) / 62);
+    const int nb = (int)((Lb + 63) / 64);
     const dim3 g(grid), b(NT);
     const LineDc dc{V, ld, j, p, part};
     if (L.seg <= 8) hipLaunchKernelGGL(k_line_spmv_dc<8>, g, b, 0, s, L, lsv, p, w, nb, stop_col, col, dc);
