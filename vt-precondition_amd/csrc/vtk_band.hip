@@ -29,7 +29,7 @@ namespace vtk {
 // for the SpMV gathers, and one launch replaces two.  Rows another workgroup owns are
 // recomputed from that row's own V_k, w_{j-1}, w_j: the x-halo lines xa-1 and xb and the v-halo
 // rows v0-1, v0+LP -- no per-step boundary copies between workgroups.  w cycles through three
-// buffers (w_{j-1}, w_j read, w_{j+1} written).  7 waves; lane tid <-> row v = v0 - 8 + tid
+// buffers (w_{j-1}, w_j read, w_{j+1} written).  7 waves; lane tid <-> row v = v0 - 16 + tid
 // (8-row BJ blocks stay lane-aligned); ~79 KB LDS: two workgroups per CU, whose update / SpMV /
 // dots phases overlap.
 // ------------------------------------------------------------------------------------------
@@ -88,6 +88,12 @@ template <int OPT> __device__ __forceinline__ void band_sync() {
     if constexpr (OPT & 8) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else __syncthreads();
 }
+// lane tid <-> row v0 - BAND_OFF + tid: 16 rows (128 B) ahead of the part's first row, so that a
+// wave's 64 rows are one aligned 512-B run of every row vector (four cache lines; with 8, the BJ
+// blocks' minimum, five: round 6), the 8-row BJ blocks lane-aligned, the v-halo rows at tid
+// BAND_OFF - 1 and BAND_OFF + LP (LP + 2 BAND_OFF <= BAND_T)
+constexpr int BAND_OFF = 16;
+static_assert(BAND_LP + 2 * BAND_OFF <= BAND_T && BAND_OFF % 8 == 0, "band geometry");
 template <int WU, int J, int VMODE = 0, bool GH = true, int OPT = 0>
 __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe<OPT>()))) void k_band_step(BandK a) {
     constexpr int BAND_RS = BAND_T;
@@ -109,10 +115,10 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
     const int L = a.L, X = a.X, H = a.H_parts, LP = L / H;
     const int b = band_block(a.opt, H), R = (int)gridDim.x / H, rb = b / H, h = b % H, v0 = h * LP;
     const int xa = (int)((int64_t)rb * X / R), xb = (int)((int64_t)(rb + 1) * X / R);
-    const int v = v0 - 8 + tid;
+    const int v = v0 - BAND_OFF + tid;
     const int wrapL = (X - 1) * L;   // |column - row| of a periodic x-coupling across the wrap
-    const bool own = tid >= 8 && tid < 8 + LP;
-    const bool upd = tid >= 7 && tid <= LP + 8 && v >= 0 && v < L;   // owned rows and the v-halo rows
+    const bool own = tid >= BAND_OFF && tid < BAND_OFF + LP;
+    const bool upd = tid >= BAND_OFF - 1 && tid <= LP + BAND_OFF && v >= 0 && v < L;   // owned rows and the v-halo rows
     constexpr bool LSV = VMODE >= 1, CANON = VMODE == 2;
     const int ii = lane & 7;
     // LSV: the lane's x-coupling values (position v in every line)
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
     auto stage = [&](double *vb) {
         if (own) {
 #pragma unroll
-            for (int k = 0; k <= J; ++k) vb[k * BAND_LP + tid - 8] = vreg[k];
+            for (int k = 0; k <= J; ++k) vb[k * BAND_LP + tid - BAND_OFF] = vreg[k];
         }
     };
     auto slot = [&](int y) { return ((y - xa + 1) & 3) * BAND_RS; };
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
         const int64_t lrow = (int64_t)(work ? x : xa) * L;
         const int64_t row = lrow + (own ? v : v0);
         // the SpMV operands of line x (independent of the update): codes, dictionary, values, m
-        const int64_t q = row >> 6, q0 = (lrow + v0 - 8 + 64 * wv) >> 6;
+        const int64_t q = row >> 6, q0 = (lrow + v0 - BAND_OFF + 64 * wv) >> 6;
         const int l64 = (int)(row & 63);
         uint32_t word = 0u;
         int dv = 0;
@@ -360,7 +366,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                 int64_t cxm, cxp;
                 const int ord = __builtin_amdgcn_readfirstlane(
                     canon_order_xv(x, 0, a.n, L, X, GH && a.ghost ? a.left_blk : -1, cxm, cxp, a.xord));
-                const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + 8;   // ring offset of line x
+                const int sx = ((x - xa + 1) & 3) * BAND_RS - v0 + BAND_OFF;   // ring offset of line x
                 // the three orders the lines take (interior / first line / last line of one rank),
                 // straight-line: every lane reads its five operands (a clamped row off its own
                 // rows), the absent v -+ 1 terms are skipped by selects -- the same additions in
@@ -371,8 +377,8 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                 const bool sl = a.canon == 2 && (ord == P_MID || ord == P_FIRST || ord == P_LAST);   // uniform
                 if (sl) {
                     const int vv = own ? v : v0;
-                    const double t0 = tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + 8 + vv];
-                    const double t4 = tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + 8 + vv];
+                    const double t0 = tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + BAND_OFF + vv];
+                    const double t4 = tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + BAND_OFF + vv];
                     const double t2 = drow * ring[sx + vv];
                     const double t1 = tv0 * ring[sx + vv - 1];
                     const double t3 = tv1 * ring[sx + vv + 1];
@@ -405,8 +411,8 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                 for (int e = 0; e < 5; ++e) {
                     const int kind = (ord >> (3 * e)) & 7;   // uniform
                     if (!sl && own) {
-                        if (kind == 0) sacc += tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + 8 + v];
-                        else if (kind == 4) sacc += tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + 8 + v];
+                        if (kind == 0) sacc += tx0 * ring[((x - xa) & 3) * BAND_RS - v0 + BAND_OFF + v];
+                        else if (kind == 4) sacc += tx1 * ring[((x - xa + 2) & 3) * BAND_RS - v0 + BAND_OFF + v];
                         else if (kind == 2) sacc += drow * ring[sx + v];
                         else if (kind == 1) {
                             if (v > 0) {
@@ -440,7 +446,7 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
                         else if (t < 0 && t >= -L) { rel = -1; vc = t + L; }
                         else if (t >= L) { rel = -1; vc = t - wrapL; }   // column in line X-1, row in line 0
                         else { rel = 1; vc = t + wrapL; }                // column in line 0, row in line X-1
-                        const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + 8];
+                        const double xv = ring[((x - xa + 1 + rel) & 3) * BAND_RS + vc - v0 + BAND_OFF];
                         double dk;
                         if constexpr (LSV) dk = rel != 0 ? (rel > 0 ? tx1 : tx0) : (vc == v ? drow : (vc > v ? tv1 : tv0));
                         else dk = d[k];
@@ -453,14 +459,14 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
             const double z = bj_trim_group<8>(own ? sacc : 0.0, lane, sub, sup, mrow);
             if (own) {
                 st_wt(a.w_out + row, z);
-                wbuf[tid - 8] = z;
+                wbuf[tid - BAND_OFF] = z;
             }
             band_sync<OPT>();
             // 3. dots of the part's rows of line x: wave wv owns items wv, wv + 7, wv + 14 (item
             //    k <= j: s_k, z_k; j + 1: |p|^2, p.w, |w|^2), lanes stride the rows.  Items
             //    outer: each item's loop streams one basis row against p and w (rows outer with
             //    p, w read once per row for all items measured slower: 1268-1285 vs 1296 it/s)
-            const double *pr = ring + slot(x) + 8;
+            const double *pr = ring + slot(x) + BAND_OFF;
 #pragma unroll
             for (int u = 0; u < BAND_IT; ++u) {
                 const int itm = wv + BAND_W * u;
