@@ -224,3 +224,45 @@ def test_distributed_line_jacobi_matches_single_rank(tmp_path, case, world, seg)
         assert abs(int(z["inner"]) - ref.inner_iters) <= 1
         x[int(z["rb"]):int(z["re"])] = z["x"]
     assert np.linalg.norm(x - ref.x) / np.linalg.norm(ref.x) <= 1e-10
+
+
+class _FakeCtx:
+    """Stands in for vtkrylov.Context in init_rccl: rank 0's unique id, every rank's comm_init."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.init_args = None
+
+    def unique_id(self):
+        assert self.rank == 0, "only rank 0 creates the RCCL unique id"
+        return bytes((7 * i + 3) % 256 for i in range(128))
+
+    def comm_init(self, rank, world, uid):
+        self.init_args = (rank, world, uid)
+
+
+def _rccl_uid_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vtkrylov import comm
+    ctx = _FakeCtx(rank)
+    comm.init_rccl(ctx, rank, world)
+    r, w, uid = ctx.init_args
+    with open(os.path.join(outdir, f"uid{rank}.bin"), "wb") as f:
+        f.write(bytes([r, w]) + uid)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_init_rccl_broadcasts_rank0_unique_id(tmp_path, world):
+    """bench.py's N>1 set-up (vtkrylov.comm.init_rccl over the gloo group the launcher makes):
+    every rank calls vtk_comm_init with its own rank, the world size and rank 0's 128-byte RCCL
+    unique id -- the host half of the RCCL path the driver's multi-GPU run is the first to use."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rccl_uid_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = bytes((7 * i + 3) % 256 for i in range(128))
+    for r in range(world):
+        got = (tmp_path / f"uid{r}.bin").read_bytes()
+        assert got[0] == r and got[1] == world and got[2:] == want, r
