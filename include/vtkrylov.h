@@ -172,12 +172,12 @@ int vtk_ctx_synchronize(vtk_ctx *ctx);
  * with and without a byte-saving form).  Each key is seeded from the environment variable
  * VTK_<KEY in upper case> once, when the context is created; the library reads its environment
  * nowhere else (fail_step is a test hook: this rank fails its DCGS2 step of that index in the
- * first cycle, vtk_gmres).  Keys: band, band_lsv, sell_canon, band_canon, band_opt, band_l2pf_rows, lsv_ring,
+ * first cycle, vtk_gmres).  Keys: band, band_lsv, sell_canon, band_canon, band_opt, band_long_rows, lsv_ring,
  * prof_perj, comm_solo, auto_band, grid4, c4_fused, g4_ring, g4_gr, g4_fast, line_fuse, cyc_ring,
  * fail_step.
  * VTK_ERR_ARG for an unknown key; a VTK_<KEY> variable of a key removed in round 5 draws a
  * warning on stderr at context creation and is otherwise ignored.  (ABI 5; fail_step ABI 6;
- * band_l2pf_rows round 6: band_opt bit 3 only on ranks of at least that many rows) */
+ * band_long_rows round 6: band_opt bits 3 and 4 only on ranks of at least that many rows) */
 int vtk_ctx_set_tuning(vtk_ctx *ctx, const char *key, int value);
 int vtk_ctx_get_tuning(vtk_ctx *ctx, const char *key, int *value);
 /* rank 0 creates the 128-byte RCCL unique id; the caller broadcasts it (any transport) */

@@ -288,7 +288,7 @@ def test_band_step_variants(vk_lib, gpu, name):
     b = twin.rhs(p.n)
     xr, ir, sr = _solve(vk_lib, gpu, A, M, b, True, restart=20)
     assert ir == 0
-    with gpu.tuning(band_l2pf_rows=0):   # bit 3 at these sizes too (by default only >= 16M rows)
+    with gpu.tuning(band_long_rows=0):   # bits 3, 4 at these sizes too (by default only >= 16M rows)
         _band_variants(vk_lib, gpu, A, M, b, xr, sr)
     M.close()
     A.close()

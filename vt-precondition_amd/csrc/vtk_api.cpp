@@ -80,7 +80,7 @@ int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
 struct TuneKey { const char *name; int Tuning::*mem; };
 constexpr TuneKey TUNE_KEYS[] = {
     {"band", &Tuning::band}, {"band_lsv", &Tuning::band_lsv}, {"sell_canon", &Tuning::sell_canon},
-    {"band_canon", &Tuning::band_canon}, {"band_opt", &Tuning::band_opt}, {"band_l2pf_rows", &Tuning::band_l2pf_rows},
+    {"band_canon", &Tuning::band_canon}, {"band_opt", &Tuning::band_opt}, {"band_long_rows", &Tuning::band_long_rows},
     {"lsv_ring", &Tuning::lsv_ring},
     {"prof_perj", &Tuning::prof_perj}, {"comm_solo", &Tuning::comm_solo}, {"auto_band", &Tuning::auto_band},
     {"grid4", &Tuning::grid4}, {"c4_fused", &Tuning::c4_fused}, {"g4_ring", &Tuning::g4_ring},
@@ -1242,11 +1242,12 @@ int dcgs2_cycle(Solver &s, const int *stop, volatile int *mirror, hipEvent_t *ev
     // the band step's variant bits exist for the line-separable, canonical-row instantiations (one
     // rank: launch_band_one_rank; across ranks with ghost lines: launch_band_ghost, round 6): every
     // other launch, and the partial count its successor reads, takes the base grid
-    // bit 3 (the LDS-DMA prefetch of J > BAND_PF) pays only on long basis vectors: on smaller ones
-    // (C2, the C3 slabs) more of the basis stays in the Infinity Cache between steps and the DMA's
-    // issue and L2 over-fetch cost more than the latency it hides (band_l2pf_rows, vtk_internal.hpp)
+    // bits 3 (the LDS-DMA prefetch of J > BAND_PF) and 4 (the alternating walk) pay only on long
+    // basis vectors: on smaller ones (C2, the C3 slabs) more of the basis stays in the Infinity
+    // Cache between steps, so the DMA's issue and L2 over-fetch cost more than the latency it hides
+    // and the halo lines' second read hits anyway (band_long_rows, vtk_internal.hpp)
     const int band_opt = band_lsv && s.A->lsv_canon && band_canon
-                             ? (n >= c->tune.band_l2pf_rows ? c->tune.band_opt : c->tune.band_opt & ~8)
+                             ? (n >= c->tune.band_long_rows ? c->tune.band_opt : c->tune.band_opt & ~(8 | 16))
                              : 0;
     // the band step's matrix bytes: SELL codes + dictionary + (values: 8 B per row from D, or
     // the SELL values)

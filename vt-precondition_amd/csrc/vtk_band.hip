@@ -520,7 +520,14 @@ __global__ __launch_bounds__(BAND_T) __attribute__((amdgpu_waves_per_eu(band_wpe
 
 // the one-rank production instantiations (canonical rows, line-separable values) with the
 // variant bits of a.opt; WPC3 only where the LDS of three workgroups fits (J <= BAND_J3)
-template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipStream_t s) {
+// SPF (bit 0) only at the step indices where it measured faster: in-process A/B, round 6, on the
+// final kernels (profiles/r06_band_bits_ab.json): j = 0 -12 us, j = 3, 4 -3 us each at C3; j = 1, 2
+// +2 / +5 us, j = 6-12 +6 ... +20 us each (the operands' registers held across the SpMV + dots);
+// the same signs on C2 and the C3 slabs
+template <int J> constexpr bool band_spf_j() { return J == 0 || J == 3 || J == 4; }
+template <int J> static void launch_band_one_rank(const BandK &a0, int grid, hipStream_t s) {
+    BandK a = a0;
+    if constexpr (!band_spf_j<J>()) a.opt &= ~1;
     const dim3 g(grid), blk(BAND_T);
     // L2PF where the registers hold no next line (J > BAND_PF).  In-process A/B (C3, round 6): j13-j17
     // 745-925 -> 709-875 us, j18 991 -> 970; with the register prefetch (J <= 12, two lines ahead)
@@ -541,13 +548,16 @@ template <int J> static void launch_band_one_rank(const BandK &a, int grid, hipS
 // third workgroup per CU at low j, no LDS-DMA prefetch at high j), which the one-rank slab
 // projections (--comm-solo: no ghost lines) did not see.  The ghost lines' update operands come from
 // the ghost buffer in load(); the DMA prefetch skips them (l2_prefetch's ghostl)
-template <int J> static void launch_band_ghost(const BandK &a, int grid, hipStream_t s) {
+template <int J> static void launch_band_ghost(const BandK &a0, int grid, hipStream_t s) {
+    BandK a = a0;
+    if constexpr (!band_spf_j<J>()) a.opt &= ~1;
     const dim3 g(grid), blk(BAND_T);
     if constexpr (J > BAND_PF) {
         if (a.opt & 8) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 9>), g, blk, 0, s, a); return; }
     }
     if constexpr (J <= BAND_J3) {
         if ((a.opt & 3) == 3) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 3>), g, blk, 0, s, a); return; }
+        if ((a.opt & 3) == 2) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 2>), g, blk, 0, s, a); return; }
     }
     if constexpr (J > BAND_J3 && J <= BAND_PF) {
         if (a.opt & 1) { hipLaunchKernelGGL((k_band_step<5, J, 2, true, 1>), g, blk, 0, s, a); return; }

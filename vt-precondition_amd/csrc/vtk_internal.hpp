@@ -184,9 +184,11 @@ struct Tuning {
                               // bit 3, LDS-DMA L2 prefetch for J > BAND_PF: j13-j18 -21..-50 us each;
                               // bit 4, odd line ranges walk backwards: 39.98 -> 39.81 ms, C3/8 slab
                               // 6.652 vs 6.676 ms (neutral).  Since round 6 also across ranks)
-    int band_l2pf_rows = 16000000;   // band_opt bit 3 only on basis vectors of >= this many rows (in-process
-                              // A/B, round 6, bit 3 on vs off: C3 20M rows 39.30 vs 39.78 ms; C3/2 slab
-                              // 10M 20.20 vs 20.09; C2 5M 10.98 vs 10.86; C3/8 slab 2.5M 6.53 vs 6.51)
+    int band_long_rows = 16000000;   // band_opt bits 3 and 4 only on basis vectors of >= this many rows
+                              // (in-process A/B, round 6: bit 3 on vs off, C3 20M rows 39.30 vs 39.78 ms,
+                              // C3/2 slab 10M 20.20 vs 20.09, C2 5M 10.98 vs 10.86, C3/8 slab 2.5M 6.53
+                              // vs 6.51; bit 4 on vs off, C3 39.24 vs 39.34, C3/2 20.13 vs 20.00, C3/4
+                              // 11.02 vs 10.95, C2 10.92 vs 10.87)
     int lsv_ring = 2048;      // > 0: the line path's table SpMV with x staged through LDS, ~that many
                               // workgroups (in-process A/B, C3 line solve: 8.64 -> 8.26 ms; 167 -> 105 us)
     int prof_perj = 0;        // profile class per band step index (band_step_jNN)
